@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""bench.py -- Mpixel-disparities/s of the MI355X semi-global matcher.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched once per GPU by torch.distributed.run.  One step = one pass of
+the hot path over one stereo pair per GPU (pairs shard one per GPU, SURVEY.md
+section 8e), inputs already resident in HBM, followed by the RCCL gather of
+the disparity maps to rank 0 when N > 1.  Rank 0 prints ONE JSON line.
+
+Metric (BASELINE.json): V*W*H*D / t in Mpixel-disparities/s, V = views
+aggregated.  Default workload = BASELINE.json configs[1] ("config 2"):
+1242x375, D=128, census 9x7 + 8-path SGM + WTA, left view (V=1).
+
+roofline: the dominant kernel (largest share of the per-step kernel time),
+its algorithmic bytes per launch (DESIGN.md "Roofline") over its average
+launch duration, measured with HIP events recorded by libsgm_hip.so around
+every launch on the stream that launch runs on (sgm_set_profiling), in a
+second pass of the same K steps right after the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpixel-disparities/s, 8-path SGM @ KITTI 1242×375 D=128; 1→8 GPU scaling"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
+
+CONFIGS = {
+    "k128": dict(h=375, w=1242, D=128, views=1,
+                 workload="config2: KITTI 1242x375 D=128, census 9x7 + Hamming cost + 8-path "
+                          "SGM + WTA/uniqueness/sub-pixel, left view (V=1), 1 pair per GPU"),
+    "k128lr": dict(h=375, w=1242, D=128, views=2,
+                   workload="KITTI 1242x375 D=128, both views + LR check (V=2), 1 pair per GPU"),
+    "hd256": dict(h=1080, w=1920, D=256, views=2,
+                  workload="config3: 1920x1080 D=256, 8-path SGM + LR check (V=2), 1 pair per GPU"),
+    "4k256": dict(h=2160, w=3840, D=256, views=2,
+                  workload="3840x2160 D=256, 8-path SGM + LR check (V=2), 1 pair per GPU"),
+}
+
+# Algorithmic HBM bytes per pixel-disparity element per launch (DESIGN.md
+# "Roofline"): f32 volumes, each read or written once.
+BYTES_PER_ELEM = {"init": 8, "acc": 12, "final": 12, "store": 8, "cost_h": 4, "cost_v": 8}
+BYTES_PER_PIXEL = {"census": 9, "lr": 12}
+
+
+def algorithmic_bytes(name: str, elems: float) -> float:
+    if name.startswith("sweep_"):
+        return BYTES_PER_ELEM[name.rsplit("_", 1)[1]] * elems
+    if name in BYTES_PER_ELEM:
+        return BYTES_PER_ELEM[name] * elems
+    return BYTES_PER_PIXEL.get(name, 0) * elems
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="k128", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=3,
+                    help="frames of the CPU baseline sample (median reported)")
+    ap.add_argument("--no-profile-pass", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    cfg = CONFIGS[args.config]
+    h, w, D, views = cfg["h"], cfg["w"], cfg["D"], cfg["views"]
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from stereo_matching_amd import SGM, synthetic
+
+    # one synthetic pair per rank (weak scaling: per-GPU work is fixed)
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=rank)
+    d_left = torch.from_numpy(left).to(dev)
+    d_right = torch.from_numpy(right).to(dev)
+    d_out = torch.empty((h, w), dtype=torch.float32, device=dev)
+    gather = [torch.empty_like(d_out) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    sgm = SGM(h, w, 1, D, views=views, device=local)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        sgm.process_device(d_left.data_ptr(), d_right.data_ptr(), d_out.data_ptr(),
+                           stream=stream.cuda_stream)
+        if world > 1:
+            dist.gather(d_out, gather_list=gather, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    def timed_steps(k):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    elapsed = timed_steps(args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    units = float(world) * views * h * w * D * args.steps
+    value = units / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # per-kernel durations: HIP events around every launch, same K steps
+    roofline = None
+    kernels = {}
+    if not args.no_profile_pass:
+        sgm.set_profiling(True)
+        timed_steps(args.steps)
+        prof = sgm.get_profile()
+        sgm.set_profiling(False)
+        for name, (n, total_ms, elems) in prof.items():
+            kernels[name] = dict(launches=n, avg_us=round(total_ms / n * 1e3, 2),
+                                 share_per_step_ms=round(total_ms / args.steps, 4),
+                                 algo_bytes=algorithmic_bytes(name, elems))
+        if kernels:
+            dom = max(kernels, key=lambda k: kernels[k]["share_per_step_ms"])
+            kd = kernels[dom]
+            achieved = kd["algo_bytes"] / (kd["avg_us"] * 1e-6) / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    with open(pmc) as fh:
+                        traffic = json.load(fh).get(args.config, {}).get(dom)
+                except (OSError, ValueError):
+                    traffic = None
+            roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "algo_bytes_per_launch": kd["algo_bytes"], "avg_launch_us": kd["avg_us"]}
+            sweep_ms = sum(v["share_per_step_ms"] for k, v in kernels.items()
+                           if k.startswith("sweep_"))
+            if sweep_ms > 0:
+                roofline["aggregation_set"] = {
+                    "kernels": "8 path sweeps per view (serial sum of event times; two chains run "
+                               "concurrently)",
+                    "algo_bytes_per_step": sum(v["algo_bytes"] * v["launches"] / args.steps
+                                               for k, v in kernels.items()
+                                               if k.startswith("sweep_")),
+                    "kernel_ms_per_step": round(sweep_ms, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        oracle.build()
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        oracle.set_threads(threads)
+        ts = []
+        for _ in range(max(1, args.cpu_frames)):
+            t0 = time.perf_counter()
+            oracle.process(left, right, D, views=views)
+            ts.append(time.perf_counter() - t0)
+        tmed = statistics.median(ts)
+        cpu = {"value": round(views * h * w * D / tmed / 1e6, 2), "unit": "Mpixel-disparities/s",
+               "cores": oracle.max_threads(), "kind": "port",
+               "sample": f"{len(ts)} full frames of the same workload ({w}x{h} D={D}, V={views}) "
+                         f"through oracle/sgm_oracle.c (C restatement, OpenMP placement of the "
+                         f"reference), median {tmed:.3f} s/frame"}
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 1), "unit": "Mpixel-disparities/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": cfg["workload"], "width": w, "height": h, "max_disp": D,
+                       "views": views, "pairs_per_gpu": 1, "global_batch": world,
+                       "parallelism": f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0"},
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+        }
+        print(json.dumps(rec))
+    sgm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * sgm_hip.h -- C-ABI of libsgm_hip.so, the MI355X-native semi-global matcher.
+ *
+ * This library replaces the reference's dormant CUDA backend (gpu_sgm/,
+ * class GPU_SGM, gpu_sgm/inc/SGM.cuh:23-62) and the CPU hot path it mirrors
+ * (class SGM : Solver, inc/SGM.h:10-26, inc/Solver.h:23-70).  Plain C: plain
+ * pointers and sizes, no STL, no OpenCV, no torch types.  The C++ class
+ * surface with the reference's signatures (include/sgm_amd/SGM.h) and the
+ * Python mirror (stereo_matching_amd/) are thin layers over these entry
+ * points; INTEGRATION.md shows how the ROS node binds it.
+ *
+ * Semantics follow src/SGM.cpp / src/Solver.cpp bit-for-bit:
+ * float32 costs, P1=10, P2=100, uniqueness 0.7, LR threshold 1.0, invalid
+ * disparity D+1.  The reference's domain d in {32,64,128} (Solver.cpp:10) is
+ * widened to 256; raw WTA disparities are therefore uint16 (the reference's
+ * uchar would wrap D+1 = 257).
+ *
+ * Threading: a handle is bound to one device and is not thread-safe (one
+ * frame at a time, like the reference object, Solver.h:29-30).  Use one
+ * handle per device/thread.
+ */
+#ifndef SGM_HIP_H
+#define SGM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGM_HIP_VERSION 1
+
+/* Status codes (the reference only asserts, Solver.cpp:6-10; GPU errors were
+ * printed and ignored, gpu_sgm/inc/cuda_inc.cuh:4-9 -- here they are returned). */
+enum {
+    SGM_OK = 0,
+    SGM_ERR_INVALID_ARG = 1,   /* a reference assert would have fired */
+    SGM_ERR_OUT_OF_MEMORY = 2,
+    SGM_ERR_HIP = 3,           /* HIP runtime error; see sgm_last_error() */
+    SGM_ERR_NO_DEVICE = 4
+};
+
+/* Path directions, numbered like the reference's L1..L8 (src/SGM.cpp:81-369). */
+enum {
+    SGM_DIR_L1 = 0, /* left -> right        */
+    SGM_DIR_L2 = 1, /* right -> left        */
+    SGM_DIR_L3 = 2, /* top -> down          */
+    SGM_DIR_L4 = 3, /* down -> top          */
+    SGM_DIR_L5 = 4, /* left-top -> right-down  */
+    SGM_DIR_L6 = 5, /* right-top -> left-down  */
+    SGM_DIR_L7 = 6, /* left-down -> right-top  */
+    SGM_DIR_L8 = 7  /* right-down -> left-top  */
+};
+
+typedef struct sgm_params {
+    int height;        /* input image rows (before decimation)      Solver(h,..) */
+    int width;         /* input image cols                           Solver(.,w,..) */
+    int scale;         /* 1 or 2: decimation (Solver.cpp:8,12-13; SGM.cpp:40-61) */
+    int max_disp;      /* D in {32,64,128,256} (Solver.cpp:10, widened)          */
+    int p1;            /* 10  (SGM.cpp:27) */
+    int p2;            /* 100 (SGM.cpp:28) */
+    float uniqueness;  /* 0.7 UNIQUE_RATIO (inc/Solver.h:14) */
+    float lr_max_diff; /* 1.0 LR_CHECK_DIS (inc/Solver.h:16) */
+    int blur;          /* 1: pre-blur as Solver.cpp:124-125 (pinned formula); 0: off */
+    int views;         /* 2: left+right views + LR check (SGM.cpp:32-818); 1: left view only */
+} sgm_params;
+
+typedef struct sgm_handle sgm_handle;
+
+/* Fills p with the reference defaults for SGM(h, w, s, d) (node.cpp:49). */
+int sgm_default_params(sgm_params *p, int h, int w, int s, int d);
+
+/* Allocates every device buffer up front, as the reference constructors do
+ * (Solver.cpp:18-27, SGM.cpp:7-24).  device = HIP ordinal. */
+int sgm_create(const sgm_params *p, int device, sgm_handle **out);
+int sgm_destroy(sgm_handle *h);
+const char *sgm_last_error(const sgm_handle *h);
+/* Working (decimated) size: rows = height/scale, cols = width/scale. */
+int sgm_get_size(const sgm_handle *h, int *rows, int *cols, int *max_disp);
+/* Bytes of device memory the handle holds. */
+size_t sgm_device_bytes(const sgm_handle *h);
+
+/*
+ * SGM::process(l, r, sky, sky_beta) (src/SGM.cpp:32-826, :829-834) up to and
+ * including the LR check, on HOST buffers; synchronous.
+ *   left/right : u8, height x width, row pitch in bytes
+ *   sky_l/sky_r: u8 masks on the working grid (rows x cols), 255 = sky; may be
+ *                NULL (Solver.cpp:146)
+ *   out        : f32 rows x cols, LR-checked sub-pixel disparity
+ *                (filtered_disp after SGM.cpp:818), invalid = D+1; with
+ *                views == 1 it is the left sub-pixel map (SGM.cpp:443)
+ *   raw_disp   : optional u16 rows x cols, left WTA disparity (SGM.cpp:411-415)
+ */
+int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
+                const uint8_t *sky_l, const uint8_t *sky_r, int sky_pitch,
+                float *out, int out_pitch, uint16_t *raw_disp);
+
+/* Same on DEVICE buffers, enqueued on `stream` (a hipStream_t; NULL = the
+ * handle's own stream).  Returns after enqueueing; the caller synchronises. */
+int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+                       const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
+                       float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream);
+
+/* post_filter() (Solver.cpp:600-649) on a host rows x cols f32 map, in place:
+ * 5x5 median fill + speckle removal, single-thread semantics.  Runs on the
+ * host (outside the north-star hot path). */
+int sgm_post_filter_host(float *disp, int rows, int cols, int max_disp, int scale);
+
+/* ---- per-kernel timing (HIP events recorded around every launch) ---- */
+
+typedef struct sgm_kernel_stat {
+    char name[32];      /* kernel class, e.g. "sweep_L3_acc" */
+    int launches;       /* completed launches since the last read */
+    double total_ms;    /* sum of event-measured durations */
+    double elems;       /* pixel-disparity elements touched per launch */
+} sgm_kernel_stat;
+
+/* enable != 0: every subsequent launch is bracketed by two HIP events on the
+ * stream it runs on.  Off by default. */
+int sgm_set_profiling(sgm_handle *h, int enable);
+/* Synchronises the handle's device, folds all pending event pairs into the
+ * per-class statistics, copies up to max entries to out, sets *count, and
+ * resets the statistics. */
+int sgm_get_profile(sgm_handle *h, sgm_kernel_stat *out, int max, int *count);
+
+/* ---- stage entry points (host buffers, synchronous), for parity tests ---- */
+
+/* Decimation + optional pre-blur + CT_pts on ONE image (cost.cpp:99-129).
+ * img: height x width (full size, pitch bytes); ct: rows x cols u64. */
+int sgm_stage_census(sgm_handle *h, const uint8_t *img, int pitch, uint64_t *ct);
+/* build_dsi_from_table[_beta] + filters (Solver.cpp:143-248, 296-368).
+ * view 0 = left, 1 = right; filters bit 1 = horizontal, bit 2 = vertical.
+ * cost: rows x cols x D f32. */
+int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr,
+                   const uint8_t *sky, int view, int filters, float *cost);
+/* One path DP over a cost volume (SGM.cpp:81-369): L (rows x cols x D) and
+ * minL (rows x cols). */
+int sgm_stage_path(sgm_handle *h, int dir, const float *cost, float *L, float *minL);
+/* 8 paths + aggregation + WTA + uniqueness + sub-pixel (SGM.cpp:81-443). */
+int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float *sub);
+/* LR check (SGM.cpp:803-818): out = checked copy of fl. */
+int sgm_stage_lr(sgm_handle *h, const float *fl, const float *fr, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,189 @@
+"""ctypes front end of the CPU oracle (oracle/sgm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() (as the
+checker) and bench.py's cpu_baseline leg.  The product package
+``stereo_matching_amd`` never imports this module.
+
+Parity status: "parity unpinned" (see sgm_oracle.h and DESIGN.md): the
+reference is unbuildable in this image and ships no golden vectors.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_sgm.so")
+_lib = None
+
+L1, L2, L3, L4, L5, L6, L7, L8 = range(8)
+
+
+def build(force: bool = False) -> str:
+    """Compile liboracle_sgm.so with the Makefile next to this file."""
+    if force or not os.path.exists(_LIB_PATH) or (
+        os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(os.path.join(_HERE, f))
+                                          for f in ("sgm_oracle.c", "sgm_oracle.h", "Makefile"))):
+        subprocess.run(["make", "-s", "-C", _HERE, "liboracle_sgm.so"], check=True)
+    return _LIB_PATH
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("disp", "disp_beta", "sub", "sub_beta", "lr", "final_disp")]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        I = ctypes.c_int
+        F = ctypes.c_float
+        L.orc_blur.argtypes = [P, P, I, I]
+        L.orc_census.argtypes = [P, P, I, I, I]
+        L.orc_dsi.argtypes = [P, P, P, P, I, I, I, I, I]
+        L.orc_hfilter.argtypes = [P, I, I, I, I]
+        L.orc_vfilter.argtypes = [P, I, I, I, I]
+        L.orc_path.argtypes = [P, P, P, I, I, I, I, I, I]
+        L.orc_aggregate.argtypes = [P, P, I, I, I]
+        L.orc_wta.argtypes = [P, P, I, I, I, F]
+        L.orc_subpixel.argtypes = [P, P, P, I, I, I]
+        L.orc_lr_check.argtypes = [P, P, I, I, I, I, F]
+        L.orc_post_filter.argtypes = [P, I, I, I, I]
+        L.orc_process.argtypes = [P, P, P, P, I, I, I, I, I, I, F, F, I, I, ctypes.POINTER(_Result)]
+        L.orc_process.restype = I
+        L.orc_max_threads.restype = I
+        L.orc_set_threads.argtypes = [I]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def blur(img):
+    img = _c(img, np.uint8)
+    out = np.empty_like(img)
+    lib().orc_blur(_p(img), _p(out), img.shape[0], img.shape[1])
+    return out
+
+
+def census(img, scale=1):
+    img = _c(img, np.uint8)
+    out = np.empty(img.shape, np.uint64)
+    lib().orc_census(_p(img), _p(out), img.shape[0], img.shape[1], scale)
+    return out
+
+
+def dsi(ctl, ctr, D, scale=1, view=0, sky=None):
+    ctl = _c(ctl, np.uint64)
+    ctr = _c(ctr, np.uint64)
+    H, W = ctl.shape
+    sky = None if sky is None else _c(sky, np.uint8)
+    out = np.empty((H, W, D), np.float32)
+    lib().orc_dsi(_p(ctl), _p(ctr), _p(sky), _p(out), H, W, D, scale, view)
+    return out
+
+
+def hfilter(cost, win):
+    c = np.array(cost, dtype=np.float32, copy=True, order="C")
+    H, W, D = c.shape
+    lib().orc_hfilter(_p(c), H, W, D, win)
+    return c
+
+
+def vfilter(cost, win):
+    c = np.array(cost, dtype=np.float32, copy=True, order="C")
+    H, W, D = c.shape
+    lib().orc_vfilter(_p(c), H, W, D, win)
+    return c
+
+
+def path(cost, direction, P1=10, P2=100):
+    cost = _c(cost, np.float32)
+    H, W, D = cost.shape
+    L = np.empty_like(cost)
+    m = np.empty((H, W), np.float32)
+    lib().orc_path(_p(cost), _p(L), _p(m), H, W, D, direction, P1, P2)
+    return L, m
+
+
+def aggregate(Ls):
+    Ls = [_c(x, np.float32) for x in Ls]
+    H, W, D = Ls[0].shape
+    arr = (ctypes.c_void_p * 8)(*[x.ctypes.data for x in Ls])
+    S = np.empty_like(Ls[0])
+    lib().orc_aggregate(ctypes.cast(arr, ctypes.c_void_p), _p(S), H, W, D)
+    return S
+
+
+def wta(S, uniq=0.7):
+    S = _c(S, np.float32)
+    H, W, D = S.shape
+    d = np.empty((H, W), np.int32)
+    lib().orc_wta(_p(S), _p(d), H, W, D, uniq)
+    return d
+
+
+def subpixel(disp, S):
+    S = _c(S, np.float32)
+    disp = _c(disp, np.int32)
+    H, W, D = S.shape
+    out = np.empty((H, W), np.float32)
+    lib().orc_subpixel(_p(disp), _p(S), _p(out), H, W, D)
+    return out
+
+
+def lr_check(FL, FR, D, scale=1, lr_dis=1.0):
+    FL = np.array(FL, dtype=np.float32, copy=True, order="C")
+    FR = _c(FR, np.float32)
+    H, W = FL.shape
+    lib().orc_lr_check(_p(FL), _p(FR), H, W, D, scale, lr_dis)
+    return FL
+
+
+def post_filter(F, D, scale=1):
+    F = np.array(F, dtype=np.float32, copy=True, order="C")
+    H, W = F.shape
+    lib().orc_post_filter(_p(F), H, W, D, scale)
+    return F
+
+
+def process(left, right, D, scale=1, sky_l=None, sky_r=None, P1=10, P2=100,
+            uniq=0.7, lr_dis=1.0, blur=True, views=2):
+    """Whole SGM::process (src/SGM.cpp:32-826).  Returns a dict of HW arrays."""
+    left = _c(left, np.uint8)
+    right = _c(right, np.uint8)
+    h, w = left.shape
+    H, W = h // scale, w // scale
+    sky_l = None if sky_l is None else _c(sky_l, np.uint8)
+    sky_r = None if sky_r is None else _c(sky_r, np.uint8)
+    out = {"disp": np.empty((H, W), np.int32), "sub": np.empty((H, W), np.float32)}
+    if views >= 2:
+        out.update(disp_beta=np.empty((H, W), np.int32), sub_beta=np.empty((H, W), np.float32),
+                   lr=np.empty((H, W), np.float32), final=np.empty((H, W), np.float32))
+    r = _Result(_p(out["disp"]), _p(out.get("disp_beta")), _p(out["sub"]),
+                _p(out.get("sub_beta")), _p(out.get("lr")), _p(out.get("final")))
+    rc = lib().orc_process(_p(left), _p(right), _p(sky_l), _p(sky_r), h, w, scale, D, P1, P2,
+                           uniq, lr_dis, int(bool(blur)), views, ctypes.byref(r))
+    if rc != 0:
+        raise ValueError("orc_process rejected its arguments")
+    return out
+
+
+def max_threads() -> int:
+    return lib().orc_max_threads()
+
+
+def set_threads(n: int) -> None:
+    lib().orc_set_threads(n)

@@ -1,0 +1,539 @@
+/*
+ * sgm_oracle.c -- CPU restatement of hilbertw/stereo_matching's CPU SGM path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see sgm_oracle.h): the parity checker for tests/,
+ * __graft_entry__.smoke() and the timed CPU baseline of bench.py.  Never
+ * linked into, loaded by, or called from the product library.
+ *
+ * PARITY STATUS: "parity unpinned" -- the reference is unbuildable here
+ * (needs OpenCV + ROS headers, inc/global.h:11-20) and ships no golden
+ * vectors; see sgm_oracle.h and DESIGN.md section "Oracle".
+ *
+ * OpenMP placement mirrors the reference so the timed
+ * baseline has the reference's parallel structure; every parallel loop writes
+ * disjoint outputs, so results do not depend on the thread count.
+ */
+#include "sgm_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* OpenCV's MIN/MAX macros as used by the reference (src/SGM.cpp:96-108). */
+#define ORC_MIN(a, b) ((a) > (b) ? (b) : (a))
+#define ORC_MAX(a, b) ((a) < (b) ? (b) : (a))
+
+typedef long long i64;
+
+int orc_max_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+void orc_set_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+/* ------------------------------------------------------------------ blur */
+
+static int reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        else i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+/* cv::GaussianBlur(src, dst, Size(3,3), 2, 1) -- src/Solver.cpp:124-125.
+ * Pinned formula (OpenCV 3.x createSeparableLinearFilter 8U fixed-point
+ * branch): row kernel round(256*g(sigma=2)) = {82,93,82}, column kernel
+ * round(256*g(sigma=1)) = {70,116,70}, int32 intermediate, output
+ * sat_u8((acc + (1<<15)) >> 16), BORDER_REFLECT_101. */
+void orc_blur(const uint8_t *src, uint8_t *dst, int H, int W)
+{
+    static const int kx[3] = {82, 93, 82};
+    static const int ky[3] = {70, 116, 70};
+    int *rows = (int *)malloc(sizeof(int) * (size_t)H * (size_t)W);
+    for (int i = 0; i < H; ++i) {
+        const uint8_t *p = src + (i64)i * W;
+        for (int j = 0; j < W; ++j) {
+            int a = p[reflect101(j - 1, W)], b = p[j], c = p[reflect101(j + 1, W)];
+            rows[(i64)i * W + j] = kx[0] * a + kx[1] * b + kx[2] * c;
+        }
+    }
+    for (int i = 0; i < H; ++i) {
+        const int *r0 = rows + (i64)reflect101(i - 1, H) * W;
+        const int *r1 = rows + (i64)i * W;
+        const int *r2 = rows + (i64)reflect101(i + 1, H) * W;
+        for (int j = 0; j < W; ++j) {
+            int acc = ky[0] * r0[j] + ky[1] * r1[j] + ky[2] * r2[j];
+            int v = (acc + (1 << 15)) >> 16;
+            dst[(i64)i * W + j] = (uint8_t)(v > 255 ? 255 : v);
+        }
+    }
+    free(rows);
+}
+
+/* ---------------------------------------------------------------- census */
+
+/* CT_pts, src/cost.cpp:99-129: window (WIN_H/scale) x (WIN_W/scale)
+ * (inc/Solver.h:10-11, Solver.cpp:127-128), MSB-first, centre skipped,
+ * coordinates clamped to the image edge, strict '>' against the centre. */
+void orc_census(const uint8_t *img, uint64_t *ct, int H, int W, int scale)
+{
+    const int win_h = 7 / scale, win_w = 9 / scale;
+#pragma omp parallel for
+    for (int v = 0; v < H; ++v) {
+        for (int u = 0; u < W; ++u) {
+            uint64_t value = 0;
+            const uint8_t ctr = img[(i64)v * W + u];
+            for (int i = -win_h / 2; i <= win_h / 2; ++i) {
+                int y = ORC_MAX(v + i, 0);
+                y = ORC_MIN(y, H - 1);
+                for (int j = -win_w / 2; j <= win_w / 2; ++j) {
+                    if (i == 0 && j == 0) continue;
+                    int x = ORC_MAX(u + j, 0);
+                    x = ORC_MIN(x, W - 1);
+                    value = (value << 1) | (uint64_t)(img[(i64)y * W + x] > ctr);
+                }
+            }
+            ct[(i64)v * W + u] = value;
+        }
+    }
+}
+
+/* hamming_cost, src/cost.cpp:132-144 (bit loop == popcount). */
+static inline int hamming(uint64_t a, uint64_t b)
+{
+    return __builtin_popcountll(a ^ b);
+}
+
+/* ------------------------------------------------------------------- DSI */
+
+void orc_dsi(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+             float *cost, int H, int W, int D, int scale, int view)
+{
+#pragma omp parallel for
+    for (int i = 0; i < H; ++i) {
+        for (int j = 0; j < W; ++j) {
+            i64 bias = ((i64)i * W + j) * D;
+            if (sky && sky[(i64)i * W + j] == 255) {
+                /* Solver.cpp:165-178 / 219-232 */
+                for (int d = 0; d < D; ++d) cost[bias + d] = d == 0 ? 0.0f : 999999.0f;
+            } else if (view == 0) {
+                /* Solver.cpp:182-190: d_bk = max(j - d/scale, 0) */
+                for (int d = 0; d < D; ++d) {
+                    int d_bk = ORC_MAX(j - d / scale, 0);
+                    cost[bias + d] = (float)hamming(ctl[(i64)i * W + j], ctr[(i64)i * W + d_bk]);
+                }
+            } else {
+                /* Solver.cpp:236-244: d_bk = min(j + d/scale, W-1) */
+                for (int d = 0; d < D; ++d) {
+                    int d_bk = ORC_MIN(j + d / scale, W - 1);
+                    cost[bias + d] = (float)hamming(ctl[(i64)i * W + d_bk], ctr[(i64)i * W + j]);
+                }
+            }
+        }
+    }
+}
+
+/* -------------------------------------------------------- in-place IIRs */
+
+/* cost_horizontal_filter, src/Solver.cpp:296-330, literally (sequential in
+ * the reference; rows are independent so the restatement may parallelise). */
+void orc_hfilter(float *cost, int H, int W, int D, int win)
+{
+    const i64 index_step = (i64)(win / 2 + 1) * D;
+#pragma omp parallel for
+    for (int i = 0; i < H; ++i) {
+        for (int d = 0; d < D; ++d) {
+            float sum = 0;
+            i64 index = (i64)i * W * D + d;
+            for (int j = 0; j < win; ++j) {
+                sum += cost[index];
+                index += D;
+            }
+            for (int j = win / 2; j < W - win / 2; ++j) {
+                cost[index - index_step] = sum / win;
+                if (j == W - win / 2 - 1) break;
+                sum += cost[index];
+                sum -= cost[index - (i64)win * D];
+                index += D;
+            }
+        }
+    }
+}
+
+/* cost_vertical_filter, src/Solver.cpp:333-368, literally. */
+void orc_vfilter(float *cost, int H, int W, int D, int win)
+{
+    const i64 step = (i64)W * D;
+    const i64 index_step = (i64)(win / 2 + 1) * step;
+#pragma omp parallel for
+    for (int j = 0; j < W; ++j) {
+        for (int d = 0; d < D; ++d) {
+            float sum = 0;
+            i64 index = (i64)j * D + d;
+            for (int i = 0; i < win; ++i) {
+                sum += cost[index];
+                index += step;
+            }
+            for (int i = win / 2; i < H - win / 2; ++i) {
+                cost[index - index_step] = sum / win;
+                if (i == H - win / 2 - 1) break;
+                sum += cost[index];
+                sum -= cost[index - (i64)win * step];
+                index += step;
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------- path DPs */
+
+/* One pixel of one path, src/SGM.cpp:93-117 (identical body in all eight
+ * directions): prev == NULL means the path starts here. */
+static inline void dp_pixel(const float *c, float *l, const float *prev, float min_prev,
+                            int D, float P1, float P2, float *min_out)
+{
+    float m = FLT_MAX;
+    for (int d = 0; d < D; ++d) {
+        int d_sub_1 = ORC_MAX(d - 1, 0);
+        int d_plus_1 = ORC_MIN(d + 1, D - 1);
+        float v;
+        if (!prev) {
+            v = c[d];
+        } else {
+            v = ORC_MIN(prev[d], prev[d_sub_1] + P1);
+            v = ORC_MIN(v, prev[d_plus_1] + P1);
+            v = ORC_MIN(v, min_prev + P2);
+            v += (c[d] - min_prev);
+        }
+        l[d] = v;
+        if (v < m) m = v;
+    }
+    *min_out = m;
+}
+
+void orc_path(const float *cost, float *L, float *minL, int H, int W, int D,
+              int dir, int P1i, int P2i)
+{
+    const float P1 = (float)P1i, P2 = (float)P2i;
+#define PIX(i, j) (((i64)(i) * W + (j)))
+#define STEP(i, j, pi, pj, start)                                                      \
+    do {                                                                               \
+        i64 q = PIX(i, j);                                                             \
+        if (start) dp_pixel(cost + q * D, L + q * D, NULL, 0.f, D, P1, P2, minL + q);  \
+        else {                                                                         \
+            i64 p = PIX(pi, pj);                                                       \
+            dp_pixel(cost + q * D, L + q * D, L + p * D, minL[p], D, P1, P2, minL + q);\
+        }                                                                              \
+    } while (0)
+
+    switch (dir) {
+    case ORC_L1: /* src/SGM.cpp:82-119, omp over rows */
+#pragma omp parallel for
+        for (int i = 0; i < H; ++i)
+            for (int j = 0; j < W; ++j) STEP(i, j, i, j - 1, j == 0);
+        break;
+    case ORC_L2: /* src/SGM.cpp:122-159 */
+#pragma omp parallel for
+        for (int i = 0; i < H; ++i)
+            for (int j = W - 1; j >= 0; --j) STEP(i, j, i, j + 1, j == W - 1);
+        break;
+    case ORC_L3: /* src/SGM.cpp:162-199, omp over columns */
+#pragma omp parallel for
+        for (int j = 0; j < W; ++j)
+            for (int i = 0; i < H; ++i) STEP(i, j, i - 1, j, i == 0);
+        break;
+    case ORC_L4: /* src/SGM.cpp:202-239 */
+#pragma omp parallel for
+        for (int j = 0; j < W; ++j)
+            for (int i = H - 1; i >= 0; --i) STEP(i, j, i + 1, j, i == H - 1);
+        break;
+    case ORC_L5: /* src/SGM.cpp:247-305: rows in order, omp over columns */
+        for (int i = 0; i < H; ++i) {
+#pragma omp parallel for
+            for (int j = 0; j < W; ++j) STEP(i, j, i - 1, j - 1, i == 0 || j == 0);
+        }
+        break;
+    case ORC_L6:
+        for (int i = 0; i < H; ++i) {
+#pragma omp parallel for
+            for (int j = 0; j < W; ++j) STEP(i, j, i - 1, j + 1, i == 0 || j == W - 1);
+        }
+        break;
+    case ORC_L7: /* src/SGM.cpp:311-369 */
+        for (int i = H - 1; i >= 0; --i) {
+#pragma omp parallel for
+            for (int j = 0; j < W; ++j) STEP(i, j, i + 1, j - 1, i == H - 1 || j == 0);
+        }
+        break;
+    case ORC_L8:
+        for (int i = H - 1; i >= 0; --i) {
+#pragma omp parallel for
+            for (int j = 0; j < W; ++j) STEP(i, j, i + 1, j + 1, i == H - 1 || j == W - 1);
+        }
+        break;
+    default:
+        break;
+    }
+#undef STEP
+#undef PIX
+}
+
+/* ------------------------------------------------ aggregation + WTA */
+
+void orc_aggregate(const float *const *L, float *S, int H, int W, int D)
+{
+    const i64 n = (i64)H * W * D;
+#pragma omp parallel for
+    for (i64 k = 0; k < n; ++k) {
+        /* src/SGM.cpp:386-390 */
+        float s = L[0][k] + L[1][k] + L[2][k] + L[3][k];
+        s += (L[4][k] + L[5][k] + L[6][k] + L[7][k]);
+        S[k] = s;
+    }
+}
+
+/* src/SGM.cpp:373-418 (sequential in the reference; min_d and sec_min_d
+ * persist across pixels exactly as there). */
+void orc_wta(const float *S, int32_t *disp, int H, int W, int D, float uniq)
+{
+    const int invalid = D + 1;
+    float min_cost = FLT_MAX, sec_min_cost = FLT_MAX;
+    int min_d = invalid, sec_min_d = invalid;
+    for (int i = 0; i < H; ++i) {
+        for (int j = 0; j < W; ++j) {
+            min_cost = FLT_MAX;
+            const float *s = S + ((i64)i * W + j) * D;
+            for (int d = 0; d < D; ++d) {
+                if (s[d] < min_cost) {
+                    min_cost = s[d];
+                    min_d = d;
+                }
+            }
+            sec_min_cost = FLT_MAX;
+            for (int d = 0; d < D; ++d) {
+                if (s[d] < sec_min_cost && s[d] != min_cost) {
+                    sec_min_cost = s[d];
+                    sec_min_d = d;
+                }
+            }
+            if (min_cost / sec_min_cost > uniq && abs(min_d - sec_min_d) > 1)
+                disp[(i64)i * W + j] = invalid;
+            else
+                disp[(i64)i * W + j] = min_d;
+        }
+    }
+}
+
+/* compute_subpixel, src/Solver.cpp:569-597. */
+void orc_subpixel(const int32_t *disp, const float *S, float *out, int H, int W, int D)
+{
+#pragma omp parallel for
+    for (int i = 0; i < H; ++i) {
+        for (int j = 0; j < W; ++j) {
+            int d = disp[(i64)i * W + j];
+            float r;
+            if (d > D - 1) {
+                r = (float)(D + 1);
+            } else if (!d || d == D - 1) {
+                r = (float)d;
+            } else {
+                i64 index = ((i64)i * W + j) * D + d;
+                float cost_d = S[index];
+                float cost_d_sub = S[index - 1];
+                float cost_d_plus = S[index + 1];
+                float x = d + (cost_d_sub - cost_d_plus) / (2 * (cost_d_sub + cost_d_plus - 2 * cost_d));
+                float lim = (D - 1) * 1.f;
+                r = (lim < x) ? lim : x; /* std::min(x, lim) */
+            }
+            out[(i64)i * W + j] = r;
+        }
+    }
+}
+
+/* src/SGM.cpp:803-818. */
+void orc_lr_check(float *FL, const float *FR, int H, int W, int D, int scale, float lr_dis)
+{
+    const float invalid = (float)(D + 1);
+#pragma omp parallel for
+    for (int i = 0; i < H; ++i) {
+        for (int j = 0; j < W; ++j) {
+            float *dl = FL + (i64)i * W + j;
+            if (j >= *dl) {
+                int jr = (int)(j - *dl / scale);
+                float dr = FR[(i64)i * W + jr];
+                if (fabsf(*dl - dr) > lr_dis) *dl = invalid;
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------- post filter */
+
+static int cmp_int(const void *a, const void *b)
+{
+    int x = *(const int *)a, y = *(const int *)b;
+    return (x > y) - (x < y);
+}
+
+static int uf_find(int *parent, int i)
+{
+    while (parent[i] != i) {
+        parent[i] = parent[parent[i]];
+        i = parent[i];
+    }
+    return i;
+}
+
+/* post_filter, src/Solver.cpp:600-649.  Median fill: sequential, row-major,
+ * in place, values truncated to int (std::vector<int>, :605,619).
+ * Speckle: speckle_filter_new (:514-566).  Its result is fully determined by
+ * the 4-connected components of the relation |a-b| < SPECKLE_DIS and their
+ * sizes (the union-find at :525-546 is exact when run by one thread), so any
+ * exact component labelling reproduces it; this one uses path halving. */
+void orc_post_filter(float *F, int H, int W, int D, int scale)
+{
+    const int MH = 5, MW = 5;
+    int v[25];
+    for (int i = MH / 2; i < H - MH / 2; ++i) {
+        for (int j = MW / 2; j < W - MW / 2; ++j) {
+            if (F[(i64)i * W + j] <= D - 1) continue;
+            int valid_cnt = 0;
+            for (int m = i - MH / 2; m <= i + MH / 2; ++m)
+                for (int n = j - MW / 2; n <= j + MW / 2; ++n) {
+                    float x = F[(i64)m * W + n];
+                    if (x <= D - 1) v[valid_cnt++] = (int)x;
+                }
+            if (valid_cnt > MW * MH / 2) {
+                qsort(v, (size_t)valid_cnt, sizeof(int), cmp_int);
+                F[(i64)i * W + j] = (float)v[valid_cnt / 2];
+            }
+        }
+    }
+
+    const int max_size = 1000 / scale, max_dis = 2;
+    const float value = (float)(D + 1);
+    const i64 n = (i64)H * W;
+    int *parent = (int *)malloc(sizeof(int) * (size_t)n);
+    int *area = (int *)calloc((size_t)n, sizeof(int));
+    for (i64 k = 0; k < n; ++k) parent[k] = (int)k;
+    for (int i = 0; i < H; ++i) {
+        for (int j = 0; j < W; ++j) {
+            i64 k = (i64)i * W + j;
+            if (j + 1 < W && fabsf(F[k] - F[k + 1]) < max_dis) {
+                int a = uf_find(parent, (int)k), b = uf_find(parent, (int)(k + 1));
+                if (a != b) parent[a] = b;
+            }
+            if (i + 1 < H && fabsf(F[k] - F[k + W]) < max_dis) {
+                int a = uf_find(parent, (int)k), b = uf_find(parent, (int)(k + W));
+                if (a != b) parent[a] = b;
+            }
+        }
+    }
+    for (i64 k = 0; k < n; ++k) area[uf_find(parent, (int)k)]++;
+    for (i64 k = 0; k < n; ++k)
+        if (area[uf_find(parent, (int)k)] <= max_size) F[k] = value;
+    free(parent);
+    free(area);
+}
+
+/* --------------------------------------------------------- whole process */
+
+int orc_process(const uint8_t *left, const uint8_t *right,
+                const uint8_t *sky_l, const uint8_t *sky_r,
+                int h, int w, int scale, int D, int P1, int P2,
+                float uniq, float lr_dis, int blur, int views, orc_result *res)
+{
+    if (h <= 0 || w <= 0 || (scale != 1 && scale != 2) || D <= 0) return -1;
+    const int H = h / scale, W = w / scale;
+    const i64 npx = (i64)H * W, nvol = npx * D;
+    if (W < 5 || H < 3) return -1;
+
+    uint8_t *l = (uint8_t *)malloc((size_t)npx), *r = (uint8_t *)malloc((size_t)npx);
+    /* decimation, src/SGM.cpp:40-61 */
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            l[(i64)i * W + j] = left[(i64)i * scale * w + (i64)j * scale];
+            r[(i64)i * W + j] = right[(i64)i * scale * w + (i64)j * scale];
+        }
+    /* build_cost_table, src/Solver.cpp:120-140 */
+    uint8_t *lb = l, *rb = r;
+    if (blur) {
+        lb = (uint8_t *)malloc((size_t)npx);
+        rb = (uint8_t *)malloc((size_t)npx);
+        orc_blur(l, lb, H, W);
+        orc_blur(r, rb, H, W);
+    }
+    uint64_t *ctl = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)npx);
+    uint64_t *ctr = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)npx);
+    orc_census(lb, ctl, H, W, scale);
+    orc_census(rb, ctr, H, W, scale);
+
+    float *cost = (float *)malloc(sizeof(float) * (size_t)nvol);
+    float *S = (float *)malloc(sizeof(float) * (size_t)nvol);
+    float *Ls[8], *mins[8];
+    for (int k = 0; k < 8; ++k) {
+        Ls[k] = (float *)malloc(sizeof(float) * (size_t)nvol);
+        mins[k] = (float *)malloc(sizeof(float) * (size_t)npx);
+    }
+    int32_t *disp = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx);
+    int32_t *disp_b = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx);
+    float *sub = (float *)malloc(sizeof(float) * (size_t)npx);
+    float *sub_b = (float *)malloc(sizeof(float) * (size_t)npx);
+
+    for (int view = 0; view < (views >= 2 ? 2 : 1); ++view) {
+        orc_dsi(ctl, ctr, view == 0 ? sky_l : sky_r, cost, H, W, D, scale, view);
+        orc_hfilter(cost, H, W, D, 5 / scale);
+        orc_vfilter(cost, H, W, D, 3 / scale);
+        for (int k = 0; k < 8; ++k) orc_path(cost, Ls[k], mins[k], H, W, D, k, P1, P2);
+        orc_aggregate((const float *const *)Ls, S, H, W, D);
+        orc_wta(S, view == 0 ? disp : disp_b, H, W, D, uniq);
+        orc_subpixel(view == 0 ? disp : disp_b, S, view == 0 ? sub : sub_b, H, W, D);
+    }
+
+    if (res) {
+        if (res->disp) memcpy(res->disp, disp, sizeof(int32_t) * (size_t)npx);
+        if (res->sub) memcpy(res->sub, sub, sizeof(float) * (size_t)npx);
+        if (views >= 2) {
+            if (res->disp_beta) memcpy(res->disp_beta, disp_b, sizeof(int32_t) * (size_t)npx);
+            if (res->sub_beta) memcpy(res->sub_beta, sub_b, sizeof(float) * (size_t)npx);
+            float *lr = (float *)malloc(sizeof(float) * (size_t)npx);
+            memcpy(lr, sub, sizeof(float) * (size_t)npx);
+            orc_lr_check(lr, sub_b, H, W, D, scale, lr_dis);
+            if (res->lr) memcpy(res->lr, lr, sizeof(float) * (size_t)npx);
+            if (res->final_disp) {
+                orc_post_filter(lr, H, W, D, scale);
+                memcpy(res->final_disp, lr, sizeof(float) * (size_t)npx);
+            }
+            free(lr);
+        }
+    }
+
+    for (int k = 0; k < 8; ++k) {
+        free(Ls[k]);
+        free(mins[k]);
+    }
+    free(cost); free(S); free(disp); free(disp_b); free(sub); free(sub_b);
+    free(ctl); free(ctr);
+    if (blur) { free(lb); free(rb); }
+    free(l); free(r);
+    return 0;
+}

@@ -1,0 +1,111 @@
+"""ctypes binding of libsgm_hip.so (include/sgm_hip.h).
+
+The library is the product: there is no CPU fallback.  If the shared object
+is missing or cannot be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libsgm_hip.so")
+CSRC = os.path.join(_PKG, "csrc")
+
+SGM_OK = 0
+SGM_ERR_INVALID_ARG = 1
+SGM_ERR_OUT_OF_MEMORY = 2
+SGM_ERR_HIP = 3
+SGM_ERR_NO_DEVICE = 4
+
+# Every symbol include/sgm_hip.h declares.
+EXPORTS = (
+    "sgm_default_params", "sgm_create", "sgm_destroy", "sgm_last_error", "sgm_get_size",
+    "sgm_device_bytes", "sgm_process", "sgm_process_device", "sgm_post_filter_host",
+    "sgm_stage_census", "sgm_stage_cost", "sgm_stage_path", "sgm_stage_aggregate",
+    "sgm_stage_lr", "sgm_set_profiling", "sgm_get_profile",
+)
+
+
+class SGMError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"libsgm_hip error {code}: {msg}")
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("height", ctypes.c_int), ("width", ctypes.c_int), ("scale", ctypes.c_int),
+        ("max_disp", ctypes.c_int), ("p1", ctypes.c_int), ("p2", ctypes.c_int),
+        ("uniqueness", ctypes.c_float), ("lr_max_diff", ctypes.c_float),
+        ("blur", ctypes.c_int), ("views", ctypes.c_int),
+    ]
+
+
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int),
+                ("total_ms", ctypes.c_double), ("elems", ctypes.c_double)]
+
+
+def build(force: bool = False, jobs: int = 2) -> str:
+    """Compile libsgm_hip.so for gfx950 with hipcc (csrc/Makefile)."""
+    if force:
+        subprocess.run(["make", "-s", "-C", CSRC, "clean"], check=True)
+    subprocess.run(["make", "-s", "-C", CSRC, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load libsgm_hip.so (raises if absent: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SGMError(SGM_ERR_NO_DEVICE,
+                       f"{LIB_PATH} is missing; build it with stereo_matching_amd._capi.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    I = ctypes.c_int
+    PP = ctypes.POINTER(Params)
+    L.sgm_default_params.argtypes = [PP, I, I, I, I]
+    L.sgm_create.argtypes = [PP, I, ctypes.POINTER(P)]
+    L.sgm_destroy.argtypes = [P]
+    L.sgm_last_error.argtypes = [P]
+    L.sgm_last_error.restype = ctypes.c_char_p
+    L.sgm_get_size.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)]
+    L.sgm_device_bytes.argtypes = [P]
+    L.sgm_device_bytes.restype = ctypes.c_size_t
+    L.sgm_process.argtypes = [P, P, P, I, P, P, I, P, I, P]
+    L.sgm_process_device.argtypes = [P, P, P, I, P, P, I, P, I, P, P]
+    L.sgm_post_filter_host.argtypes = [P, I, I, I, I]
+    L.sgm_stage_census.argtypes = [P, P, I, P]
+    L.sgm_stage_cost.argtypes = [P, P, P, P, I, I, P]
+    L.sgm_stage_path.argtypes = [P, I, P, P, P]
+    L.sgm_stage_aggregate.argtypes = [P, P, P, P]
+    L.sgm_stage_lr.argtypes = [P, P, P, P]
+    L.sgm_set_profiling.argtypes = [P, I]
+    L.sgm_get_profile.argtypes = [P, ctypes.POINTER(KernelStat), I, ctypes.POINTER(I)]
+    for name in EXPORTS:
+        if name not in ("sgm_last_error", "sgm_device_bytes"):
+            getattr(L, name).restype = I
+    _lib = L
+    return L
+
+
+def check(rc: int, handle=None) -> None:
+    if rc != SGM_OK:
+        msg = ""
+        if handle is not None and _lib is not None:
+            raw = _lib.sgm_last_error(handle)
+            msg = raw.decode() if raw else ""
+        raise SGMError(rc, msg)
+
+
+def default_params(h: int, w: int, s: int, d: int) -> Params:
+    p = Params()
+    check(lib().sgm_default_params(ctypes.byref(p), h, w, s, d))
+    return p

@@ -1,0 +1,594 @@
+// sgm_capi.hip -- the C-ABI of libsgm_hip.so (include/sgm_hip.h).
+//
+// Host orchestration of one frame (DESIGN.md "Frame schedule"):
+//
+//   caller stream : census L,R -> cost_h(L) -> cost_v(L) -> L1 L2 L3 L4 (S_L) --.
+//   aux0          :                      \-> L5 L6 L7 (T_L) -------------------+-> L8 FINAL(L)
+//   aux1          : cost_h(R) -> cost_v(R) -> L1 L2 L3 L4 (S_R) --.            |
+//   aux2          :                     \-> L5 L6 L7 (T_R) -------+-> L8 FINAL(R)
+//   caller stream : join -> LR check
+//
+// All device memory is allocated at sgm_create (the reference allocates its
+// scratch in the constructors, Solver.cpp:18-27 and SGM.cpp:7-24).
+#include "../../include/sgm_hip.h"
+#include "sgm_internal.h"
+
+#include <algorithm>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <new>
+#include <vector>
+
+using sgm::Geom;
+using sgm::SweepArgs;
+
+struct sgm_handle {
+    sgm_params p;
+    Geom g;
+    int device;
+    int nviews;
+    size_t bytes;
+    hipStream_t st;       // the handle's own stream (host API, stages)
+    hipStream_t aux[3];
+    hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_v1;
+    uint8_t *d_in[2];     // full-size input staging (host API)
+    uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
+    uint64_t *d_ct[2];    // census words
+    float *d_ch[2];       // horizontally filtered cost; reused as the T chain
+    float *d_c[2];        // final cost volume
+    float *d_s[2];        // S chain
+    uint16_t *d_disp[2];  // WTA disparity
+    float *d_sub[2];      // sub-pixel disparity
+    float *d_out;         // LR-checked output (host API)
+    float *d_min;         // minL (stage_path)
+    char err[512];
+    // profiling (sgm_set_profiling)
+    int profiling;
+    std::vector<hipEvent_t> ev_pool;
+    struct Pending { int cls; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<sgm_kernel_stat> stats;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int set_err(sgm_handle *h, int code, const char *fmt, ...) {
+    if (h) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(h->err, sizeof(h->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(h, expr)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err((h), e_ == hipErrorOutOfMemory ? SGM_ERR_OUT_OF_MEMORY : SGM_ERR_HIP, \
+                           "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,   \
+                           __LINE__);                                                        \
+    } while (0)
+
+bool valid_params(const sgm_params *p, char *why, size_t n) {
+    if (!p) { snprintf(why, n, "params is NULL"); return false; }
+    // Solver.cpp:6-10 (d widened to 256), plus the filter windows' minimum size.
+    if (p->height <= 0 || p->width <= 0 || p->scale <= 0 || p->max_disp <= 0) {
+        snprintf(why, n, "h, w, s, d must be > 0 (Solver.cpp:6)");
+        return false;
+    }
+    if (p->scale != 1 && p->scale != 2) { snprintf(why, n, "scale must be 1 or 2 (Solver.cpp:8)"); return false; }
+    if (p->max_disp != 32 && p->max_disp != 64 && p->max_disp != 128 && p->max_disp != 256) {
+        snprintf(why, n, "max_disp must be 32, 64, 128 or 256 (Solver.cpp:10, widened)");
+        return false;
+    }
+    const int H = p->height / p->scale, W = p->width / p->scale;
+    if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
+    if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
+    if ((size_t)H * W > (size_t)0x7fffffff) { snprintf(why, n, "image too large"); return false; }
+    return true;
+}
+
+template <typename T>
+int dalloc(sgm_handle *h, T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return SGM_OK;
+    HIPCHK(h, hipMalloc((void **)p, count * sizeof(T)));
+    h->bytes += count * sizeof(T);
+    return SGM_OK;
+}
+
+void free_all(sgm_handle *h) {
+    for (int v = 0; v < 2; ++v) {
+        (void)hipFree(h->d_in[v]); (void)hipFree(h->d_sky[v]); (void)hipFree(h->d_ct[v]);
+        (void)hipFree(h->d_ch[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
+        (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
+    }
+    (void)hipFree(h->d_out);
+    (void)hipFree(h->d_min);
+    if (h->st) (void)hipStreamDestroy(h->st);
+    for (auto &s : h->aux) if (s) (void)hipStreamDestroy(s);
+    hipEvent_t evs[] = {h->ev_ct, h->ev_c[0], h->ev_c[1], h->ev_t[0], h->ev_t[1], h->ev_v1};
+    for (auto e : evs) if (e) (void)hipEventDestroy(e);
+    for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    h->pending.clear();
+    h->ev_pool.clear();
+}
+
+hipEvent_t pool_event(sgm_handle *h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int stat_class(sgm_handle *h, const char *name, double elems) {
+    for (size_t k = 0; k < h->stats.size(); ++k)
+        if (!strncmp(h->stats[k].name, name, sizeof(h->stats[k].name))) return (int)k;
+    sgm_kernel_stat st{};
+    snprintf(st.name, sizeof(st.name), "%s", name);
+    st.elems = elems;
+    h->stats.push_back(st);
+    return (int)h->stats.size() - 1;
+}
+
+// Launch `fn` on `st`; with profiling on, bracket it with pooled events.
+template <typename F>
+hipError_t timed(sgm_handle *h, const char *name, double elems, hipStream_t st, F &&fn) {
+    if (!h->profiling) return fn();
+    hipEvent_t a = pool_event(h), b = pool_event(h);
+    if (!a || !b) return hipErrorOutOfMemory;
+    hipError_t e = hipEventRecord(a, st);
+    if (e == hipSuccess) e = fn();
+    if (e == hipSuccess) e = hipEventRecord(b, st);
+    h->pending.push_back({stat_class(h, name, elems), a, b});
+    return e;
+}
+
+const char *kDirName[8] = {"L1", "L2", "L3", "L4", "L5", "L6", "L7", "L8"};
+const char *kModeName[4] = {"store", "init", "acc", "final"};
+
+hipError_t sweep(sgm_handle *h, int dir, int mode, const SweepArgs &a, hipStream_t st) {
+    char name[32];
+    snprintf(name, sizeof(name), "sweep_%s_%s", kDirName[dir], kModeName[mode]);
+    const double elems = (double)h->g.H * h->g.W * h->g.D;
+    return timed(h, name, elems, st, [&] { return sgm::launch_sweep(dir, mode, a, h->g, st); });
+}
+
+SweepArgs sweep_args(const sgm_handle *h) {
+    SweepArgs a{};
+    a.p1 = (float)h->p.p1;
+    a.p2 = (float)h->p.p2;
+    a.uniq = h->p.uniqueness;
+    return a;
+}
+
+// The 8-path aggregation of one view: S chain (L1..L4) on `s_st`, T chain
+// (L5..L7) on `t_st`, then L8 fused with the sum, WTA, uniqueness and
+// sub-pixel on `s_st`.  t buffer may alias the (dead) horizontally filtered
+// cost volume.
+int aggregate_view(sgm_handle *h, const float *cost, float *S, float *T, uint16_t *disp, float *sub,
+                   hipStream_t s_st, hipStream_t t_st, hipEvent_t ev_src, hipEvent_t ev_t) {
+    SweepArgs a = sweep_args(h);
+    a.cost = cost;
+    HIPCHK(h, hipStreamWaitEvent(t_st, ev_src, 0));
+    // T chain: T = ((L5 + L6) + L7)
+    a.acc_out = T;
+    HIPCHK(h, sweep(h, SGM_DIR_L5, sgm::SWEEP_INIT, a, t_st));
+    a.acc_in = T;
+    HIPCHK(h, sweep(h, SGM_DIR_L6, sgm::SWEEP_ACC, a, t_st));
+    HIPCHK(h, sweep(h, SGM_DIR_L7, sgm::SWEEP_ACC, a, t_st));
+    HIPCHK(h, hipEventRecord(ev_t, t_st));
+    // S chain: S = ((L1 + L2) + L3) + L4
+    a.acc_in = nullptr;
+    a.acc_out = S;
+    HIPCHK(h, sweep(h, SGM_DIR_L1, sgm::SWEEP_INIT, a, s_st));
+    a.acc_in = S;
+    HIPCHK(h, sweep(h, SGM_DIR_L2, sgm::SWEEP_ACC, a, s_st));
+    HIPCHK(h, sweep(h, SGM_DIR_L3, sgm::SWEEP_ACC, a, s_st));
+    HIPCHK(h, sweep(h, SGM_DIR_L4, sgm::SWEEP_ACC, a, s_st));
+    // join, then total = S + (T + L8) -> WTA -> sub-pixel
+    HIPCHK(h, hipStreamWaitEvent(s_st, ev_t, 0));
+    a.acc_in = T;
+    a.s_in = S;
+    a.acc_out = nullptr;
+    a.disp = disp;
+    a.sub = sub;
+    HIPCHK(h, sweep(h, SGM_DIR_L8, sgm::SWEEP_FINAL, a, s_st));
+    return SGM_OK;
+}
+
+int cost_view(sgm_handle *h, int view, const uint8_t *sky, int sky_pitch, hipStream_t st) {
+    const double elems = (double)h->g.H * h->g.W * h->g.D;
+    HIPCHK(h, timed(h, "cost_h", elems, st, [&] {
+               return sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky, sky_pitch, view, 1, h->g,
+                                         h->d_ch[view], st);
+           }));
+    HIPCHK(h, timed(h, "cost_v", elems, st, [&] {
+               return sgm::launch_cost_v(h->d_ch[view], h->d_c[view], 1, h->g, st);
+           }));
+    return SGM_OK;
+}
+
+int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+              const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch, float *d_out,
+              int out_pitch, uint16_t *d_raw, hipStream_t st) {
+    const Geom g = h->g;
+    int rc;
+    const double npx = (double)g.H * g.W;
+    HIPCHK(h, timed(h, "census", npx, st, [&] {
+               return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st);
+           }));
+    HIPCHK(h, timed(h, "census", npx, st, [&] {
+               return sgm::launch_census(d_right, pitch, g, h->p.blur, h->d_ct[1], st);
+           }));
+    HIPCHK(h, hipEventRecord(h->ev_ct, st));
+    if (h->nviews == 2) {
+        HIPCHK(h, hipStreamWaitEvent(h->aux[1], h->ev_ct, 0));
+        if ((rc = cost_view(h, 1, d_sky_r, sky_pitch, h->aux[1])) != SGM_OK) return rc;
+        HIPCHK(h, hipEventRecord(h->ev_c[1], h->aux[1]));
+    }
+    if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
+    HIPCHK(h, hipEventRecord(h->ev_c[0], st));
+    if ((rc = aggregate_view(h, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
+                             h->aux[0], h->ev_c[0], h->ev_t[0])) != SGM_OK)
+        return rc;
+    if (h->nviews == 2) {
+        if ((rc = aggregate_view(h, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
+                                 h->aux[1], h->aux[2], h->ev_c[1], h->ev_t[1])) != SGM_OK)
+            return rc;
+        HIPCHK(h, hipEventRecord(h->ev_v1, h->aux[1]));
+        HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
+        HIPCHK(h, timed(h, "lr", npx, st, [&] {
+                   return sgm::launch_lr(h->d_sub[0], h->d_sub[1], d_out, out_pitch,
+                                         h->p.lr_max_diff, g, st);
+               }));
+    } else {
+        HIPCHK(h, hipMemcpy2DAsync(d_out, (size_t)out_pitch * sizeof(float), h->d_sub[0],
+                                   (size_t)g.W * sizeof(float), (size_t)g.W * sizeof(float), g.H,
+                                   hipMemcpyDeviceToDevice, st));
+    }
+    if (d_raw)
+        HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
+                                 hipMemcpyDeviceToDevice, st));
+    return SGM_OK;
+}
+
+int copy_in_image(sgm_handle *h, uint8_t *dst, const uint8_t *src, int pitch) {
+    HIPCHK(h, hipMemcpy2DAsync(dst, (size_t)h->p.width, src, (size_t)pitch, (size_t)h->p.width,
+                               (size_t)h->p.height, hipMemcpyHostToDevice, h->st));
+    return SGM_OK;
+}
+
+int copy_in_mask(sgm_handle *h, uint8_t *dst, const uint8_t *src, int pitch) {
+    HIPCHK(h, hipMemcpy2DAsync(dst, (size_t)h->g.W, src, (size_t)pitch, (size_t)h->g.W,
+                               (size_t)h->g.H, hipMemcpyHostToDevice, h->st));
+    return SGM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
+    if (!p) return SGM_ERR_INVALID_ARG;
+    p->height = h;
+    p->width = w;
+    p->scale = s;
+    p->max_disp = d;
+    p->p1 = 10;              // SGM.cpp:27
+    p->p2 = 100;             // SGM.cpp:28
+    p->uniqueness = 0.7f;    // inc/Solver.h:14
+    p->lr_max_diff = 1.0f;   // inc/Solver.h:16
+    p->blur = 1;             // Solver.cpp:124-125
+    p->views = 2;            // SGM.cpp:448-818
+    return SGM_OK;
+}
+
+int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
+    if (!out) return SGM_ERR_INVALID_ARG;
+    *out = nullptr;
+    char why[256];
+    if (!valid_params(p, why, sizeof(why))) {
+        fprintf(stderr, "sgm_create: %s\n", why);
+        return SGM_ERR_INVALID_ARG;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SGM_ERR_NO_DEVICE;
+    if (device < 0 || device >= ndev) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(device);
+
+    sgm_handle *h = new (std::nothrow) sgm_handle();
+    if (!h) return SGM_ERR_OUT_OF_MEMORY;
+    h->p = *p;
+    h->device = device;
+    h->g.scale = p->scale;
+    h->g.H = p->height / p->scale;
+    h->g.W = p->width / p->scale;
+    h->g.D = p->max_disp;
+    h->nviews = p->views;
+
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    const size_t nvol = npx * h->g.D;
+    const size_t nin = (size_t)p->height * p->width;
+    int rc = SGM_OK;
+    do {
+        if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
+        for (auto &s : h->aux)
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
+        if (rc) break;
+        hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1], &h->ev_v1};
+        for (auto e : evs)
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { rc = SGM_ERR_HIP; break; }
+        if (rc) break;
+        for (int v = 0; v < 2 && !rc; ++v) {
+            if ((rc = dalloc(h, &h->d_in[v], nin))) break;
+            if ((rc = dalloc(h, &h->d_sky[v], npx))) break;
+            if ((rc = dalloc(h, &h->d_ct[v], npx))) break;
+        }
+        for (int v = 0; v < h->nviews && !rc; ++v) {
+            if ((rc = dalloc(h, &h->d_ch[v], nvol))) break;
+            if ((rc = dalloc(h, &h->d_c[v], nvol))) break;
+            if ((rc = dalloc(h, &h->d_s[v], nvol))) break;
+            if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
+            if ((rc = dalloc(h, &h->d_sub[v], npx))) break;
+        }
+        if (!rc && h->nviews == 1) {  // stage_lr needs a second sub-pixel map
+            rc = dalloc(h, &h->d_sub[1], npx);
+        }
+        if (!rc) rc = dalloc(h, &h->d_out, npx);
+        if (!rc) rc = dalloc(h, &h->d_min, npx);
+    } while (0);
+    if (rc) {
+        fprintf(stderr, "sgm_create: %s\n", h->err[0] ? h->err : "HIP stream/event creation failed");
+        free_all(h);
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return SGM_OK;
+}
+
+int sgm_destroy(sgm_handle *h) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    {
+        DeviceGuard guard(h->device);
+        (void)hipDeviceSynchronize();
+        free_all(h);
+    }
+    delete h;
+    return SGM_OK;
+}
+
+const char *sgm_last_error(const sgm_handle *h) { return h ? h->err : "null handle"; }
+
+int sgm_get_size(const sgm_handle *h, int *rows, int *cols, int *max_disp) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (rows) *rows = h->g.H;
+    if (cols) *cols = h->g.W;
+    if (max_disp) *max_disp = h->g.D;
+    return SGM_OK;
+}
+
+size_t sgm_device_bytes(const sgm_handle *h) { return h ? h->bytes : 0; }
+
+int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+                       const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
+                       float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!d_left || !d_right || !d_out || pitch < h->p.width || out_pitch < h->g.W ||
+        ((d_sky_l || d_sky_r) && sky_pitch < h->g.W))
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process_device: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    return run_frame(h, d_left, d_right, pitch, d_sky_l, d_sky_r, sky_pitch, d_out, out_pitch,
+                     d_raw_disp, st);
+}
+
+int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
+                const uint8_t *sky_l, const uint8_t *sky_r, int sky_pitch, float *out,
+                int out_pitch, uint16_t *raw_disp) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!left || !right || !out || pitch < h->p.width || out_pitch < h->g.W ||
+        ((sky_l || sky_r) && sky_pitch < h->g.W))
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    int rc;
+    if ((rc = copy_in_image(h, h->d_in[0], left, pitch))) return rc;
+    if ((rc = copy_in_image(h, h->d_in[1], right, pitch))) return rc;
+    if (sky_l && (rc = copy_in_mask(h, h->d_sky[0], sky_l, sky_pitch))) return rc;
+    if (sky_r && (rc = copy_in_mask(h, h->d_sky[1], sky_r, sky_pitch))) return rc;
+    uint16_t *d_raw = raw_disp ? h->d_disp[0] : nullptr;  // read back below
+    if ((rc = run_frame(h, h->d_in[0], h->d_in[1], h->p.width, sky_l ? h->d_sky[0] : nullptr,
+                        sky_r ? h->d_sky[1] : nullptr, h->g.W, h->d_out, h->g.W, nullptr, h->st)))
+        return rc;
+    (void)d_raw;
+    HIPCHK(h, hipMemcpy2DAsync(out, (size_t)out_pitch * sizeof(float), h->d_out,
+                               (size_t)h->g.W * sizeof(float), (size_t)h->g.W * sizeof(float),
+                               h->g.H, hipMemcpyDeviceToHost, h->st));
+    if (raw_disp)
+        HIPCHK(h, hipMemcpyAsync(raw_disp, h->d_disp[0], (size_t)h->g.H * h->g.W * sizeof(uint16_t),
+                                 hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_set_profiling(sgm_handle *h, int enable) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    h->profiling = enable ? 1 : 0;
+    return SGM_OK;
+}
+
+int sgm_get_profile(sgm_handle *h, sgm_kernel_stat *out, int max, int *count) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    HIPCHK(h, hipDeviceSynchronize());
+    for (auto &p : h->pending) {
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, p.a, p.b));
+        h->stats[p.cls].launches += 1;
+        h->stats[p.cls].total_ms += ms;
+        h->ev_pool.push_back(p.a);
+        h->ev_pool.push_back(p.b);
+    }
+    h->pending.clear();
+    int n = 0;
+    for (auto &st : h->stats) {
+        if (st.launches == 0) continue;
+        if (out && n < max) out[n] = st;
+        ++n;
+    }
+    if (count) *count = out ? (n < max ? n : max) : n;
+    for (auto &st : h->stats) { st.launches = 0; st.total_ms = 0; }
+    return SGM_OK;
+}
+
+// ----------------------------------------------------------- post filter
+
+namespace {
+int uf_find(std::vector<int> &p, int i) {
+    while (p[i] != i) {
+        p[i] = p[p[i]];
+        i = p[i];
+    }
+    return i;
+}
+}  // namespace
+
+int sgm_post_filter_host(float *F, int H, int W, int D, int scale) {
+    if (!F || H <= 0 || W <= 0 || D <= 0 || scale <= 0) return SGM_ERR_INVALID_ARG;
+    // Median fill, Solver.cpp:604-630: sequential, row-major, in place,
+    // int-truncated samples, more than 12 valid samples required.
+    int v[25];
+    for (int i = 2; i < H - 2; ++i)
+        for (int j = 2; j < W - 2; ++j) {
+            if (F[(size_t)i * W + j] <= D - 1) continue;
+            int cnt = 0;
+            for (int m = i - 2; m <= i + 2; ++m)
+                for (int n = j - 2; n <= j + 2; ++n) {
+                    const float x = F[(size_t)m * W + n];
+                    if (x <= D - 1) v[cnt++] = (int)x;
+                }
+            if (cnt > 12) {
+                std::sort(v, v + cnt);
+                F[(size_t)i * W + j] = (float)v[cnt / 2];
+            }
+        }
+    // Speckle removal, Solver.cpp:514-566 (single-thread semantics): 4-connected
+    // components of |a-b| < 2 with at most 1000/scale pixels become invalid.
+    const size_t n = (size_t)H * W;
+    std::vector<int> parent(n), area(n, 0);
+    for (size_t k = 0; k < n; ++k) parent[k] = (int)k;
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            const size_t k = (size_t)i * W + j;
+            if (j + 1 < W && fabsf(F[k] - F[k + 1]) < 2) {
+                int a = uf_find(parent, (int)k), b = uf_find(parent, (int)k + 1);
+                if (a != b) parent[a] = b;
+            }
+            if (i + 1 < H && fabsf(F[k] - F[k + W]) < 2) {
+                int a = uf_find(parent, (int)k), b = uf_find(parent, (int)(k + W));
+                if (a != b) parent[a] = b;
+            }
+        }
+    for (size_t k = 0; k < n; ++k) area[uf_find(parent, (int)k)]++;
+    const int max_size = 1000 / scale;
+    for (size_t k = 0; k < n; ++k)
+        if (area[uf_find(parent, (int)k)] <= max_size) F[k] = (float)(D + 1);
+    return SGM_OK;
+}
+
+// -------------------------------------------------------------- stages
+
+int sgm_stage_census(sgm_handle *h, const uint8_t *img, int pitch, uint64_t *ct) {
+    if (!h || !img || !ct || pitch < h->p.width) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    int rc;
+    if ((rc = copy_in_image(h, h->d_in[0], img, pitch))) return rc;
+    HIPCHK(h, sgm::launch_census(h->d_in[0], h->p.width, h->g, h->p.blur, h->d_ct[0], h->st));
+    HIPCHK(h, hipMemcpyAsync(ct, h->d_ct[0], (size_t)h->g.H * h->g.W * sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+                   int view, int filters, float *cost) {
+    if (!h || !ctl || !ctr || !cost || (view != 0 && view != 1)) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
+    HIPCHK(h, hipMemcpyAsync(h->d_ct[0], ctl, npx * 8, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipMemcpyAsync(h->d_ct[1], ctr, npx * 8, hipMemcpyHostToDevice, h->st));
+    if (sky) HIPCHK(h, hipMemcpyAsync(h->d_sky[0], sky, npx, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky ? h->d_sky[0] : nullptr, h->g.W, view,
+                                 filters & 1, h->g, h->d_ch[0], h->st));
+    HIPCHK(h, sgm::launch_cost_v(h->d_ch[0], h->d_c[0], filters & 2, h->g, h->st));
+    HIPCHK(h, hipMemcpyAsync(cost, h->d_c[0], nvol * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_stage_path(sgm_handle *h, int dir, const float *cost, float *L, float *minL) {
+    if (!h || !cost || !L || dir < 0 || dir > 7) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
+    HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
+    SweepArgs a = sweep_args(h);
+    a.cost = h->d_c[0];
+    a.acc_out = h->d_s[0];
+    a.min_out = h->d_min;
+    HIPCHK(h, sgm::launch_sweep(dir, sgm::SWEEP_STORE_L, a, h->g, h->st));
+    HIPCHK(h, hipMemcpyAsync(L, h->d_s[0], nvol * 4, hipMemcpyDeviceToHost, h->st));
+    if (minL) HIPCHK(h, hipMemcpyAsync(minL, h->d_min, npx * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float *sub) {
+    if (!h || !cost) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
+    HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipEventRecord(h->ev_c[0], h->st));
+    int rc = aggregate_view(h, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], h->st,
+                            h->aux[0], h->ev_c[0], h->ev_t[0]);
+    if (rc) return rc;
+    if (disp) HIPCHK(h, hipMemcpyAsync(disp, h->d_disp[0], npx * 2, hipMemcpyDeviceToHost, h->st));
+    if (sub) HIPCHK(h, hipMemcpyAsync(sub, h->d_sub[0], npx * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_stage_lr(sgm_handle *h, const float *fl, const float *fr, float *out) {
+    if (!h || !fl || !fr || !out) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    HIPCHK(h, hipMemcpyAsync(h->d_sub[0], fl, npx * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipMemcpyAsync(h->d_sub[1], fr, npx * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, sgm::launch_lr(h->d_sub[0], h->d_sub[1], h->d_out, h->g.W, h->p.lr_max_diff, h->g, h->st));
+    HIPCHK(h, hipMemcpyAsync(out, h->d_out, npx * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+}  // extern "C"

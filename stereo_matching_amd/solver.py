@@ -1,0 +1,169 @@
+"""Python mirror of the reference's Solver/SGM class surface.
+
+Reference: inc/Solver.h:23-70 and inc/SGM.h:10-26 (constructor SGM(h, w, s, d),
+process(l, r[, sky, sky_beta]), get_disp()).  Every call goes through the
+C-ABI of libsgm_hip.so; nothing here computes disparities itself.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _u8(a, shape, what):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    if a.shape != shape:
+        raise ValueError(f"{what}: expected shape {shape}, got {a.shape}")
+    return a
+
+
+class SGM:
+    """Semi-global matcher on one MI355X (HIP device `device`).
+
+    Mirrors ``SGM(int h, int w, int s, int d)`` (src/SGM.cpp:4-29).  The
+    reference asserts s in {1, 2} and d in {32, 64, 128} (Solver.cpp:6-10);
+    here d = 256 is also accepted and invalid arguments raise SGMError.
+    """
+
+    def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0,
+                 blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
+                 uniqueness: float = 0.7, lr_max_diff: float = 1.0):
+        self._lib = lib()
+        p = _capi.default_params(h, w, s, d)
+        p.blur = int(bool(blur))
+        p.views = views
+        p.p1, p.p2 = p1, p2
+        p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
+        self.params = p
+        self.h, self.w, self.scale, self.max_disp = h, w, s, d
+        self.rows, self.cols = h // s, w // s
+        self.invalid_disp = d + 1
+        handle = ctypes.c_void_p()
+        check(self._lib.sgm_create(ctypes.byref(p), device, ctypes.byref(handle)))
+        self._h = handle
+        self.device = device
+        self._lr = np.full((self.rows, self.cols), self.invalid_disp, np.float32)
+        self._raw = np.zeros((self.rows, self.cols), np.uint16)
+        self._final = None
+
+    # ---------------------------------------------------------- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.sgm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self._lib.sgm_device_bytes(self._h))
+
+    # ------------------------------------------------------------ process
+    def process(self, img_l, img_r, sky_mask=None, sky_mask_beta=None) -> None:
+        """SGM::process (src/SGM.cpp:32-826, sky overload :829-834)."""
+        l = _u8(img_l, (self.h, self.w), "img_l")
+        r = _u8(img_r, (self.h, self.w), "img_r")
+        sl = None if sky_mask is None or np.size(sky_mask) == 0 else \
+            _u8(sky_mask, (self.rows, self.cols), "sky_mask")
+        sr = None if sky_mask_beta is None or np.size(sky_mask_beta) == 0 else \
+            _u8(sky_mask_beta, (self.rows, self.cols), "sky_mask_beta")
+        check(self._lib.sgm_process(self._h, _ptr(l), _ptr(r), self.w, _ptr(sl), _ptr(sr),
+                                    self.cols, _ptr(self._lr), self.cols, _ptr(self._raw)),
+              self._h)
+        self._final = None
+
+    def process_device(self, d_left: int, d_right: int, d_out: int, *, pitch: int | None = None,
+                       d_sky_l: int = 0, d_sky_r: int = 0, sky_pitch: int | None = None,
+                       out_pitch: int | None = None, d_raw: int = 0, stream: int = 0) -> None:
+        """Device-pointer variant (sgm_process_device): enqueue on `stream`."""
+        check(self._lib.sgm_process_device(
+            self._h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), pitch or self.w,
+            ctypes.c_void_p(d_sky_l or None), ctypes.c_void_p(d_sky_r or None),
+            sky_pitch or self.cols, ctypes.c_void_p(d_out), out_pitch or self.cols,
+            ctypes.c_void_p(d_raw or None), ctypes.c_void_p(stream or None)), self._h)
+
+    def get_disp(self) -> np.ndarray:
+        """Post-filtered disparity (inc/Solver.h:36: filtered_disp after
+        post_filter, Solver.cpp:600-649); invalid = D+1."""
+        if self._final is None:
+            f = self._lr.copy()
+            check(self._lib.sgm_post_filter_host(_ptr(f), self.rows, self.cols, self.max_disp,
+                                                 self.scale))
+            self._final = f
+        return self._final
+
+    def get_lr_disp(self) -> np.ndarray:
+        """Sub-pixel disparity after the LR check (SGM.cpp:803-818)."""
+        return self._lr
+
+    def get_raw_disp(self) -> np.ndarray:
+        """Left WTA disparity (SGM.cpp:411-415), uint16, invalid = D+1."""
+        return self._raw
+
+    # ---------------------------------------------------------- profiling
+    def set_profiling(self, enable: bool) -> None:
+        check(self._lib.sgm_set_profiling(self._h, int(bool(enable))), self._h)
+
+    def get_profile(self) -> dict:
+        """{kernel class: (launches, total_ms, elements per launch)}; resets."""
+        buf = (_capi.KernelStat * 64)()
+        n = ctypes.c_int()
+        check(self._lib.sgm_get_profile(self._h, buf, 64, ctypes.byref(n)), self._h)
+        return {buf[k].name.decode(): (buf[k].launches, buf[k].total_ms, buf[k].elems)
+                for k in range(n.value)}
+
+    # ------------------------------------------------------------- stages
+    def stage_census(self, img) -> np.ndarray:
+        img = _u8(img, (self.h, self.w), "img")
+        out = np.empty((self.rows, self.cols), np.uint64)
+        check(self._lib.sgm_stage_census(self._h, _ptr(img), self.w, _ptr(out)), self._h)
+        return out
+
+    def stage_cost(self, ctl, ctr, view=0, sky=None, filters=3) -> np.ndarray:
+        ctl = np.ascontiguousarray(ctl, np.uint64)
+        ctr = np.ascontiguousarray(ctr, np.uint64)
+        sky = None if sky is None else _u8(sky, (self.rows, self.cols), "sky")
+        out = np.empty((self.rows, self.cols, self.max_disp), np.float32)
+        check(self._lib.sgm_stage_cost(self._h, _ptr(ctl), _ptr(ctr), _ptr(sky), view, filters,
+                                       _ptr(out)), self._h)
+        return out
+
+    def stage_path(self, direction: int, cost):
+        cost = np.ascontiguousarray(cost, np.float32)
+        L = np.empty_like(cost)
+        m = np.empty((self.rows, self.cols), np.float32)
+        check(self._lib.sgm_stage_path(self._h, direction, _ptr(cost), _ptr(L), _ptr(m)),
+              self._h)
+        return L, m
+
+    def stage_aggregate(self, cost):
+        cost = np.ascontiguousarray(cost, np.float32)
+        d = np.empty((self.rows, self.cols), np.uint16)
+        f = np.empty((self.rows, self.cols), np.float32)
+        check(self._lib.sgm_stage_aggregate(self._h, _ptr(cost), _ptr(d), _ptr(f)), self._h)
+        return d, f
+
+    def stage_lr(self, fl, fr) -> np.ndarray:
+        fl = np.ascontiguousarray(fl, np.float32)
+        fr = np.ascontiguousarray(fr, np.float32)
+        out = np.empty_like(fl)
+        check(self._lib.sgm_stage_lr(self._h, _ptr(fl), _ptr(fr), _ptr(out)), self._h)
+        return out

@@ -1,0 +1,248 @@
+"""Independent numpy restatement of the reference's CPU SGM path.
+
+Written separately from oracle/sgm_oracle.c (different loop structure:
+vectorised over disparities and over the independent pixels of each sweep
+front) so that the two restatements check each other at small sizes.  Every
+float32 operation is an explicit numpy float32 op in the reference's
+association order.  Tests only; small inputs only.
+"""
+from __future__ import annotations
+
+from collections import deque
+
+import numpy as np
+
+f32 = np.float32
+FLT_MAX = np.finfo(np.float32).max
+
+
+def blur(img):
+    """Pinned cv::GaussianBlur(3x3, 2, 1) on CV_8U (src/Solver.cpp:124-125)."""
+    a = img.astype(np.int64)
+    H, W = a.shape
+
+    def refl(idx, n):
+        idx = np.where(idx < 0, -idx, idx)
+        return np.where(idx >= n, 2 * n - 2 - idx, idx) if n > 1 else np.zeros_like(idx)
+
+    cols = np.arange(W)
+    rows = np.arange(H)
+    hsum = 82 * a[:, refl(cols - 1, W)] + 93 * a + 82 * a[:, refl(cols + 1, W)]
+    acc = 70 * hsum[refl(rows - 1, H)] + 116 * hsum + 70 * hsum[refl(rows + 1, H)]
+    return np.minimum((acc + 32768) >> 16, 255).astype(np.uint8)
+
+
+def census(img, scale=1):
+    """CT_pts (src/cost.cpp:99-129) via shifted, edge-clamped copies."""
+    H, W = img.shape
+    wh, ww = 7 // scale, 9 // scale
+    out = np.zeros((H, W), np.uint64)
+    ctr = img
+    ys = np.arange(H)
+    xs = np.arange(W)
+    for di in range(-(wh // 2), wh // 2 + 1):
+        yy = np.clip(ys + di, 0, H - 1)
+        for dj in range(-(ww // 2), ww // 2 + 1):
+            if di == 0 and dj == 0:
+                continue
+            xx = np.clip(xs + dj, 0, W - 1)
+            nb = img[yy][:, xx]
+            out = (out << np.uint64(1)) | (nb > ctr).astype(np.uint64)
+    return out
+
+
+def _popcount(x):
+    x = x.astype(np.uint64)
+    c = np.zeros(x.shape, np.int64)
+    for b in range(64):
+        c += ((x >> np.uint64(b)) & np.uint64(1)).astype(np.int64)
+    return c
+
+
+def dsi(ctl, ctr, D, scale=1, view=0, sky=None):
+    H, W = ctl.shape
+    j = np.arange(W)[:, None]
+    d = np.arange(D)[None, :]
+    if view == 0:
+        idx = np.maximum(j - d // scale, 0)
+        c = _popcount(ctl[:, :, None] ^ ctr[:, idx])
+    else:
+        idx = np.minimum(j + d // scale, W - 1)
+        c = _popcount(ctl[:, idx] ^ ctr[:, :, None])
+    c = c.astype(np.float32)
+    if sky is not None:
+        m = sky == 255
+        c[m] = f32(999999)
+        c[m, 0] = f32(0)
+    return c
+
+
+def _iir_along(a, win):
+    """In-place literal IIR along axis 0 of a (n, ...) float32 array
+    (src/Solver.cpp:296-330 and :333-368 share this body)."""
+    n = a.shape[0]
+    s = np.zeros(a.shape[1:], np.float32)
+    idx = 0
+    for _ in range(win):
+        s = s + a[idx]
+        idx += 1
+    h = win // 2
+    j = h
+    while j < n - h:
+        a[idx - (h + 1)] = s / f32(win)
+        if j == n - h - 1:
+            break
+        s = s + a[idx]
+        s = s - a[idx - win]
+        idx += 1
+        j += 1
+    return a
+
+
+def hfilter(cost, win):
+    c = np.array(cost, np.float32, copy=True)
+    return np.ascontiguousarray(np.swapaxes(_iir_along(np.swapaxes(c, 0, 1), win), 0, 1))
+
+
+def vfilter(cost, win):
+    c = np.array(cost, np.float32, copy=True)
+    return _iir_along(c, win)
+
+
+def _dp(prev, min_prev, c, P1, P2):
+    D = c.shape[-1]
+    dm = np.maximum(np.arange(D) - 1, 0)
+    dp = np.minimum(np.arange(D) + 1, D - 1)
+    v = np.minimum(prev, prev[..., dm] + f32(P1))
+    v = np.minimum(v, prev[..., dp] + f32(P1))
+    v = np.minimum(v, (min_prev + f32(P2))[..., None])
+    v = v + (c - min_prev[..., None])
+    return v
+
+
+# (di, dj): the step from predecessor to pixel along the path.
+DIRS = [(0, 1), (0, -1), (1, 0), (-1, 0), (1, 1), (1, -1), (-1, 1), (-1, -1)]
+
+
+def path(cost, direction, P1=10, P2=100):
+    """src/SGM.cpp:81-369; sweeps one front at a time."""
+    H, W, D = cost.shape
+    di, dj = DIRS[direction]
+    L = np.empty_like(cost)
+    if di == 0:
+        cols = range(W) if dj > 0 else range(W - 1, -1, -1)
+        first = True
+        for j in cols:
+            if first:
+                L[:, j] = cost[:, j]
+                first = False
+            else:
+                p = L[:, j - dj]
+                L[:, j] = _dp(p, p.min(axis=-1), cost[:, j], P1, P2)
+    else:
+        rows = range(H) if di > 0 else range(H - 1, -1, -1)
+        first = True
+        for i in rows:
+            if first:
+                L[i] = cost[i]
+                first = False
+                continue
+            p_row = L[i - di]
+            out = np.empty((W, D), np.float32)
+            for j in range(W):
+                pj = j - dj
+                if pj < 0 or pj >= W:
+                    out[j] = cost[i, j]
+                else:
+                    p = p_row[pj]
+                    out[j] = _dp(p, p.min(), cost[i, j], P1, P2)
+            L[i] = out
+    return L, L.min(axis=-1)
+
+
+def aggregate(Ls):
+    s = ((Ls[0] + Ls[1]) + Ls[2]) + Ls[3]
+    return s + (((Ls[4] + Ls[5]) + Ls[6]) + Ls[7])
+
+
+def wta(S, uniq=0.7):
+    H, W, D = S.shape
+    out = np.empty((H, W), np.int32)
+    u = f32(uniq)
+    for i in range(H):
+        for j in range(W):
+            s = S[i, j]
+            m = s.min()
+            md = int(np.argmax(s == m))
+            rest = s[s != m]
+            if rest.size == 0:
+                out[i, j] = md
+                continue
+            sm = rest.min()
+            sd = int(np.argmax(s == sm))
+            out[i, j] = D + 1 if (f32(m) / f32(sm) > u and abs(md - sd) > 1) else md
+    return out
+
+
+def subpixel(disp, S):
+    H, W, D = S.shape
+    out = np.empty((H, W), np.float32)
+    for i in range(H):
+        for j in range(W):
+            d = int(disp[i, j])
+            if d > D - 1:
+                out[i, j] = D + 1
+            elif d == 0 or d == D - 1:
+                out[i, j] = d
+            else:
+                a, b, c = S[i, j, d - 1], S[i, j, d + 1], S[i, j, d]
+                x = f32(d) + (a - b) / (f32(2) * ((a + b) - f32(2) * c))
+                out[i, j] = f32(D - 1) if f32(D - 1) < x else x
+    return out
+
+
+def lr_check(FL, FR, D, scale=1, lr_dis=1.0):
+    FL = np.array(FL, np.float32, copy=True)
+    H, W = FL.shape
+    for i in range(H):
+        for j in range(W):
+            dl = FL[i, j]
+            if f32(j) >= dl:
+                jr = int(f32(j) - dl / f32(scale))
+                if abs(dl - FR[i, jr]) > f32(lr_dis):
+                    FL[i, j] = D + 1
+    return FL
+
+
+def post_filter(F, D, scale=1):
+    F = np.array(F, np.float32, copy=True)
+    H, W = F.shape
+    for i in range(2, H - 2):
+        for j in range(2, W - 2):
+            if F[i, j] <= D - 1:
+                continue
+            win = F[i - 2:i + 3, j - 2:j + 3].ravel()
+            v = sorted(int(x) for x in win if x <= D - 1)
+            if len(v) > 12:
+                F[i, j] = v[len(v) // 2]
+    seen = np.zeros((H, W), bool)
+    max_size = 1000 // scale
+    for i in range(H):
+        for j in range(W):
+            if seen[i, j]:
+                continue
+            comp = [(i, j)]
+            seen[i, j] = True
+            q = deque(comp)
+            while q:
+                a, b = q.popleft()
+                for na, nb in ((a - 1, b), (a + 1, b), (a, b - 1), (a, b + 1)):
+                    if 0 <= na < H and 0 <= nb < W and not seen[na, nb] and \
+                            abs(F[a, b] - F[na, nb]) < 2:
+                        seen[na, nb] = True
+                        comp.append((na, nb))
+                        q.append((na, nb))
+            if len(comp) <= max_size:
+                for a, b in comp:
+                    F[a, b] = D + 1
+    return F

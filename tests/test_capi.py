@@ -1,0 +1,84 @@
+"""CPU checks of the C-ABI library: it is built for gfx950, loads, exports
+every entry point include/sgm_hip.h declares, and validates arguments the way
+the reference's asserts do -- without running any kernel."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from stereo_matching_amd import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sgm_hip.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(sgm_[a-z_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_capi.LIB_PATH):
+        _capi.build()
+    return _capi.lib()
+
+
+def test_header_and_binding_agree():
+    assert header_symbols() == sorted(_capi.EXPORTS)
+
+
+def test_library_exports_every_symbol(lib):
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    for name in header_symbols():
+        assert re.search(rf"\bT {name}$", out, re.M), name
+
+
+def test_library_carries_gfx950_code_object():
+    # the embedded HIP fat binary names its offload targets
+    data = open(_capi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_default_params_are_the_reference_constants(lib):
+    p = _capi.default_params(375, 1242, 1, 128)
+    assert (p.p1, p.p2) == (10, 100)                # src/SGM.cpp:27-28
+    assert abs(p.uniqueness - 0.7) < 1e-7           # inc/Solver.h:14
+    assert p.lr_max_diff == 1.0                     # inc/Solver.h:16
+    assert p.blur == 1 and p.views == 2 and p.scale == 1 and p.max_disp == 128
+
+
+@pytest.mark.parametrize("h,w,s,d", [(375, 1242, 3, 128), (375, 1242, 1, 96), (0, 10, 1, 32),
+                                     (2, 100, 1, 32), (100, 4, 1, 32)])
+def test_invalid_arguments_rejected(lib, h, w, s, d):
+    # the reference asserts (Solver.cpp:6-10); the C-ABI returns SGM_ERR_INVALID_ARG
+    p = _capi.Params()
+    lib.sgm_default_params(ctypes.byref(p), h, w, s, d)
+    handle = ctypes.c_void_p()
+    rc = lib.sgm_create(ctypes.byref(p), 0, ctypes.byref(handle))
+    assert rc == _capi.SGM_ERR_INVALID_ARG
+    assert not handle.value
+
+
+def test_null_arguments_rejected(lib):
+    assert lib.sgm_create(None, 0, None) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_destroy(None) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_process(None, None, None, 0, None, None, 0, None, 0, None) == \
+        _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_post_filter_host(None, 1, 1, 32, 1) == _capi.SGM_ERR_INVALID_ARG
+
+
+def test_no_silent_fallback_without_gpu(lib):
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    from stereo_matching_amd import SGM, SGMError
+    with pytest.raises(SGMError):
+        SGM(375, 1242, 1, 128)
