@@ -29,6 +29,7 @@ struct sgm_handle {
     Geom g;
     int device;
     int nviews;
+    int serialize;        // SGM_SERIALIZE=1: every kernel on one stream (isolated timings)
     size_t bytes;
     hipStream_t st;       // the handle's own stream (host API, stages)
     hipStream_t aux[3];
@@ -235,6 +236,9 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
     const Geom g = h->g;
     int rc;
+    hipStream_t aux0 = h->serialize ? st : h->aux[0];
+    hipStream_t aux1 = h->serialize ? st : h->aux[1];
+    hipStream_t aux2 = h->serialize ? st : h->aux[2];
     const double npx = (double)g.H * g.W;
     HIPCHK(h, timed(h, "census", npx, st, [&] {
                return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st);
@@ -244,20 +248,20 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
            }));
     HIPCHK(h, hipEventRecord(h->ev_ct, st));
     if (h->nviews == 2) {
-        HIPCHK(h, hipStreamWaitEvent(h->aux[1], h->ev_ct, 0));
-        if ((rc = cost_view(h, 1, d_sky_r, sky_pitch, h->aux[1])) != SGM_OK) return rc;
-        HIPCHK(h, hipEventRecord(h->ev_c[1], h->aux[1]));
+        HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
+        if ((rc = cost_view(h, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
+        HIPCHK(h, hipEventRecord(h->ev_c[1], aux1));
     }
     if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
     HIPCHK(h, hipEventRecord(h->ev_c[0], st));
     if ((rc = aggregate_view(h, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
-                             h->aux[0], h->ev_c[0], h->ev_t[0])) != SGM_OK)
+                             aux0, h->ev_c[0], h->ev_t[0])) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
         if ((rc = aggregate_view(h, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
-                                 h->aux[1], h->aux[2], h->ev_c[1], h->ev_t[1])) != SGM_OK)
+                                 aux1, aux2, h->ev_c[1], h->ev_t[1])) != SGM_OK)
             return rc;
-        HIPCHK(h, hipEventRecord(h->ev_v1, h->aux[1]));
+        HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
         HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
         HIPCHK(h, timed(h, "lr", npx, st, [&] {
                    return sgm::launch_lr(h->d_sub[0], h->d_sub[1], d_out, out_pitch,
@@ -327,6 +331,10 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
     h->g.W = p->width / p->scale;
     h->g.D = p->max_disp;
     h->nviews = p->views;
+    {
+        const char *ser = getenv("SGM_SERIALIZE");
+        h->serialize = ser && ser[0] == '1';
+    }
 
     const size_t npx = (size_t)h->g.H * h->g.W;
     const size_t nvol = npx * h->g.D;

@@ -60,18 +60,26 @@ __device__ __forceinline__ float movdppf(float src) {
     return __int_as_float(movdpp<CTRL, ROW_MASK, BANK_MASK>(__float_as_int(src)));
 }
 
-// Minimum over the 64 lanes, returned wave-uniform (SGPR).  Quad, half-row
-// and row mirrors leave every lane of a row with the row minimum; the two
-// row broadcasts fold rows 0..3 into lane 63 (rows 0 and 2 are not written
-// by them and are never read afterwards).
+// Minimum over the 64 lanes, left in EVERY lane (a VGPR, no readlane on the
+// DP chain): the quad, half-row and row mirrors give each lane its row (16
+// lane) minimum; v_permlane16_swap pairs rows 0<->1 and 2<->3, and
+// v_permlane32_swap the two wave halves (gfx950).
 __device__ __forceinline__ float wave_min(float x) {
     x = fminf(x, movdppf<DPP_QP_1032>(x));
     x = fminf(x, movdppf<DPP_QP_2301>(x));
     x = fminf(x, movdppf<DPP_HALF_MIRROR>(x));
     x = fminf(x, movdppf<DPP_MIRROR>(x));
-    x = fminf(x, movdppf<DPP_BCAST15, 0xA>(x));
-    x = fminf(x, movdppf<DPP_BCAST31, 0xC>(x));
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x),
+                                                    false, false);
+    x = fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x),
+                                                    false, false);
+    return fminf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
+// Same, returned as a wave-uniform scalar.
+__device__ __forceinline__ float wave_min_u(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_min(x))));
 }
 
 __device__ __forceinline__ int wave_min_i(int x) {
@@ -163,30 +171,46 @@ hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64
 
 // ------------------------------------------------ DSI + horizontal IIR
 
-// One thread per (row, d) chain; 256/D rows per block.  The raw Hamming DSI
-// (Solver.cpp:143-248, sky override :165-178) is produced on the fly and fed
-// straight into the in-place horizontal IIR of Solver.cpp:296-330, restated
-// with a register history: with h = WIN/2 and LAG = WIN-h-1 the reference
-// writes position LAG+t at step t, adds raw[WIN+t] and subtracts the value at
-// position t, which is the step-(t-LAG) output once t >= LAG and raw before.
-template <int VIEW, int WIN>
+// One thread per (row, d) chain, R rows per block (R*D threads).  The census
+// rows of both images (and the sky row) are staged in LDS once per block; the
+// raw Hamming DSI (Solver.cpp:143-248, sky override :165-178) is produced on
+// the fly and fed straight into the in-place horizontal IIR of
+// Solver.cpp:296-330, restated with a register history: with h = WIN/2 and
+// LAG = WIN-h-1 the reference writes position LAG+t at step t, adds raw[WIN+t]
+// and subtracts the value at position t, which is the step-(t-LAG) output once
+// t >= LAG and raw before.
+constexpr int COSTH_MAX_LDS = 64 * 1024;
+
+template <int VIEW, int WIN, bool SKY, bool FILTER>
 __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
                                                      const uint64_t *__restrict__ ctr,
                                                      const uint8_t *__restrict__ sky,
-                                                     int sky_pitch, int filter, int H, int W,
-                                                     int D, int scale, float *__restrict__ out) {
-    const int rows_per_block = 256 / D;
+                                                     int sky_pitch, int H, int W, int D, int scale,
+                                                     int R, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
+    uint64_t *sr = sl + (size_t)R * W;
+    uint8_t *ss = reinterpret_cast<uint8_t *>(sr + (size_t)R * W);
+    const int row0 = blockIdx.x * R;
+    for (int idx = threadIdx.x; idx < R * W; idx += blockDim.x) {
+        const int r = idx / W, j = idx - r * W, i = row0 + r;
+        if (i < H) {
+            sl[idx] = ctl[(size_t)i * W + j];
+            sr[idx] = ctr[(size_t)i * W + j];
+            if (SKY) ss[idx] = sky[(size_t)i * sky_pitch + j];
+        }
+    }
+    __syncthreads();
     const int r = threadIdx.x / D, d = threadIdx.x - r * D;
-    const int i = blockIdx.x * rows_per_block + r;
+    const int i = row0 + r;
     if (i >= H) return;
-    const uint64_t *cl = ctl + (size_t)i * W;
-    const uint64_t *cr = ctr + (size_t)i * W;
-    const uint8_t *sk = sky ? sky + (size_t)i * sky_pitch : nullptr;
+    const uint64_t *cl = sl + (size_t)r * W;
+    const uint64_t *cr = sr + (size_t)r * W;
+    const uint8_t *sk = ss + (size_t)r * W;
     const int ds = d / scale;
     float *o = out + (size_t)i * W * D + d;
 
     auto raw = [&](int j) -> float {
-        if (sk && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
         uint64_t a, b;
         if (VIEW == 0) {
             a = cl[j];
@@ -195,10 +219,12 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
             a = cl[min(j + ds, W - 1)];
             b = cr[j];
         }
-        return (float)__popcll(a ^ b);
+        const float c = (float)__popcll(a ^ b);
+        if (SKY && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
+        return c;
     };
 
-    if (!filter) {
+    if (!FILTER) {
         for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
         return;
     }
@@ -210,7 +236,59 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
     const int T = W - 2 * HALF;
     float o1 = 0.0f, o2 = 0.0f;
-#pragma unroll 4
+    const float r0 = raw(0), r1 = raw(1);
+#pragma unroll 8
+    for (int t = 0; t < T; ++t) {
+        const float v = sum / (float)WIN;
+        o[(size_t)(LAG + t) * D] = v;
+        if (t == T - 1) break;
+        sum += raw(WIN + t);
+        float a;
+        if (LAG == 0) a = v;
+        else if (LAG == 1) a = t >= 1 ? o1 : r0;
+        else a = t >= 2 ? o2 : (t == 0 ? r0 : r1);
+        sum -= a;
+        o2 = o1;
+        o1 = v;
+    }
+    for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
+}
+
+// Fallback for rows too wide to stage in LDS (W*16 B > 64 KiB): census words
+// read straight from global memory.
+template <int VIEW, int WIN, bool SKY, bool FILTER>
+__global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__restrict__ ctl,
+                                                            const uint64_t *__restrict__ ctr,
+                                                            const uint8_t *__restrict__ sky,
+                                                            int sky_pitch, int H, int W, int D,
+                                                            int scale, float *__restrict__ out) {
+    const int rows_per_block = 256 / D;
+    const int r = threadIdx.x / D, d = threadIdx.x - r * D;
+    const int i = blockIdx.x * rows_per_block + r;
+    if (i >= H) return;
+    const uint64_t *cl = ctl + (size_t)i * W;
+    const uint64_t *cr = ctr + (size_t)i * W;
+    const uint8_t *sk = SKY ? sky + (size_t)i * sky_pitch : nullptr;
+    const int ds = d / scale;
+    float *o = out + (size_t)i * W * D + d;
+    auto raw = [&](int j) -> float {
+        if (SKY && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
+        const uint64_t a = VIEW == 0 ? cl[j] : cl[min(j + ds, W - 1)];
+        const uint64_t b = VIEW == 0 ? cr[max(j - ds, 0)] : cr[j];
+        return (float)__popcll(a ^ b);
+    };
+    if (!FILTER) {
+        for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
+        return;
+    }
+    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1;
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < WIN; ++k) sum += raw(k);
+#pragma unroll
+    for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
+    const int T = W - 2 * HALF;
+    float o1 = 0.0f, o2 = 0.0f;
     for (int t = 0; t < T; ++t) {
         const float v = sum / (float)WIN;
         o[(size_t)(LAG + t) * D] = v;
@@ -227,27 +305,56 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
 }
 
+template <int VIEW, int WIN, bool SKY, bool FILTER>
+static void launch_cost_h_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+                            int sky_pitch, Geom g, float *out, hipStream_t st) {
+    const size_t row_bytes = (size_t)g.W * (16 + (SKY ? 1 : 0));
+    int R = (int)(COSTH_MAX_LDS / row_bytes);
+    if (R > 256 / g.D) R = 256 / g.D;
+    if (R >= 1) {
+        const size_t smem = (size_t)R * row_bytes;
+        cost_h_kernel<VIEW, WIN, SKY, FILTER><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+            ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
+    } else {
+        const int rpb = 256 / g.D;
+        cost_h_global_kernel<VIEW, WIN, SKY, FILTER><<<dim3((g.H + rpb - 1) / rpb), 256, 0, st>>>(
+            ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, out);
+    }
+}
+
+template <int VIEW, int WIN>
+static void launch_cost_h_w(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+                            int sky_pitch, int filter, Geom g, float *out, hipStream_t st) {
+    if (sky) {
+        if (filter) launch_cost_h_t<VIEW, WIN, true, true>(ctl, ctr, sky, sky_pitch, g, out, st);
+        else launch_cost_h_t<VIEW, WIN, true, false>(ctl, ctr, sky, sky_pitch, g, out, st);
+    } else {
+        if (filter) launch_cost_h_t<VIEW, WIN, false, true>(ctl, ctr, sky, sky_pitch, g, out, st);
+        else launch_cost_h_t<VIEW, WIN, false, false>(ctl, ctr, sky, sky_pitch, g, out, st);
+    }
+}
+
 hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                          int sky_pitch, int view, int filter, Geom g, float *out,
                          hipStream_t st) {
-    const int rpb = 256 / g.D;
-    const dim3 grid((g.H + rpb - 1) / rpb);
-    const int f = filter ? 1 : 0;
-#define SGM_COSTH(V, WN) \
-    cost_h_kernel<V, WN><<<grid, 256, 0, st>>>(ctl, ctr, sky, sky_pitch, f, g.H, g.W, g.D, g.scale, out)
     if (view == 0) {
-        if (g.scale == 1) SGM_COSTH(0, 5); else SGM_COSTH(0, 2);
+        if (g.scale == 1) launch_cost_h_w<0, 5>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
+        else launch_cost_h_w<0, 2>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
     } else {
-        if (g.scale == 1) SGM_COSTH(1, 5); else SGM_COSTH(1, 2);
+        if (g.scale == 1) launch_cost_h_w<1, 5>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
+        else launch_cost_h_w<1, 2>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
     }
-#undef SGM_COSTH
     return hipGetLastError();
 }
 
 // ------------------------------------------------------ vertical IIR
 
 // One thread per (col, d) chain walking the rows (Solver.cpp:333-368), out of
-// place: in = horizontally filtered volume, out = final cost volume.
+// place: in = horizontally filtered volume, out = final cost volume.  The raw
+// rows the recurrence adds (raw[WIN+t]) stream through a register ring
+// VPF steps ahead of the arithmetic.
+constexpr int VPF = 16;
+
 template <int WIN>
 __global__ __launch_bounds__(256) void cost_v_kernel(const float *__restrict__ in,
                                                      float *__restrict__ out, int H, int W,
@@ -261,24 +368,37 @@ __global__ __launch_bounds__(256) void cost_v_kernel(const float *__restrict__ i
     float sum = 0.0f;
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += a[k * stride];
+    const float r0 = a[0], r1 = LAG >= 2 ? a[stride] : 0.0f;
 #pragma unroll
     for (int p = 0; p < LAG; ++p) o[p * stride] = a[p * stride];
     const int T = H - 2 * HALF;
+    float ring[VPF];
+#pragma unroll
+    for (int u = 0; u < VPF; ++u) ring[u] = a[(size_t)min(WIN + u, H - 1) * stride];
     float o1 = 0.0f, o2 = 0.0f;
-#pragma unroll 8
-    for (int t = 0; t < T; ++t) {
+    auto step = [&](int t, int u, bool refill) {
         const float v = sum / (float)WIN;
         o[(size_t)(LAG + t) * stride] = v;
-        if (t == T - 1) break;
-        sum += a[(size_t)(WIN + t) * stride];
+        const float rw = ring[u];
+        if (refill) ring[u] = a[(size_t)min(WIN + t + VPF, H - 1) * stride];
         float s;
         if (LAG == 0) s = v;
-        else if (LAG == 1) s = t >= 1 ? o1 : a[(size_t)t * stride];
-        else s = t >= 2 ? o2 : a[(size_t)t * stride];
-        sum -= s;
+        else if (LAG == 1) s = t >= 1 ? o1 : r0;
+        else s = t >= 2 ? o2 : (t == 0 ? r0 : r1);
+        sum = (sum + rw) - s;
         o2 = o1;
         o1 = v;
+    };
+    // steps 0 .. T-2 update the running sum; step T-1 only writes
+    int t0 = 0;
+    for (; t0 + VPF <= T - 1; t0 += VPF) {
+#pragma unroll
+        for (int u = 0; u < VPF; ++u) step(t0 + u, u, true);
     }
+#pragma unroll
+    for (int u = 0; u < VPF; ++u)
+        if (t0 + u < T - 1) step(t0 + u, u, false);
+    o[(size_t)(LAG + T - 1) * stride] = sum / (float)WIN;
     for (int p = LAG + T; p < H; ++p) o[(size_t)p * stride] = a[(size_t)p * stride];
 }
 
@@ -409,35 +529,36 @@ __device__ __forceinline__ float pick(const float (&x)[V], int v) {
 
 // Aggregated WTA + uniqueness (SGM.cpp:376-418) and compute_subpixel
 // (Solver.cpp:577-593) for one pixel whose total cost vector is spread over
-// the wave; results are wave-uniform.
+// the wave (d = lane*V + v); everything after the two wave minima is scalar:
+// the first index holding a value is the lowest set bit of a ballot.
+// Lanes without data hold +inf (never equal to a finite minimum).
 template <int V>
-__device__ __forceinline__ void wta_subpixel(const float (&tot)[V], int lane, int D, float uniq,
+__device__ __forceinline__ int first_index(const float (&tot)[V], float x) {
+    int best = INT_MAX;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const unsigned long long m = __ballot(tot[v] == x);
+        const int cand = m ? (int)__builtin_ctzll(m) * V + v : INT_MAX;
+        best = cand < best ? cand : best;
+    }
+    return best;
+}
+
+template <int V>
+__device__ __forceinline__ void wta_subpixel(const float (&tot)[V], int D, float uniq,
                                              int &disp_out, float &sub_out) {
-    const int e0 = lane * V;
     float lm = tot[0];
 #pragma unroll
     for (int v = 1; v < V; ++v) lm = fminf(lm, tot[v]);
-    const float m = wave_min(lm);
-    int cand = INT_MAX;
+    const float m = wave_min_u(lm);
     float ls = SGM_INF;
 #pragma unroll
-    for (int v = V - 1; v >= 0; --v) {
-        if (tot[v] == m) cand = e0 + v;
-    }
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-        if (tot[v] != m) ls = fminf(ls, tot[v]);
-    }
-    const int min_d = wave_min_i(cand);
-    const float sec = wave_min(ls);
+    for (int v = 0; v < V; ++v) ls = fminf(ls, tot[v] != m ? tot[v] : SGM_INF);
+    const float sec = wave_min_u(ls);
+    const int min_d = first_index<V>(tot, m);
     int d = min_d;
-    if (sec != SGM_INF) {
-        int scand = INT_MAX;
-#pragma unroll
-        for (int v = V - 1; v >= 0; --v) {
-            if (tot[v] == sec) scand = e0 + v;
-        }
-        const int sec_d = wave_min_i(scand);
+    if (sec != SGM_INF) {  // a second distinct value exists (else sec = FLT_MAX: ratio ~ 0)
+        const int sec_d = first_index<V>(tot, sec);
         if (m / sec > uniq && abs(min_d - sec_d) > 1) d = D + 1;
     }
     float f;
@@ -457,12 +578,12 @@ __device__ __forceinline__ void wta_subpixel(const float (&tot)[V], int lane, in
     sub_out = f;
 }
 
-constexpr int SWEEP_PF = 8;  // steps of cost / accumulator loads kept in flight
-
 // One wavefront per path; lane l holds disparities l*V .. l*V+V-1 (FULL: all
 // 64 lanes hold data, i.e. D >= 64; D = 32 uses lanes 0..31 and +inf above).
-// Loads run SWEEP_PF steps ahead of the DP through a register ring.
-template <int DIR, int V, int MODE, bool FULL>
+// Loads run PF steps ahead of the DP through a register ring.  In FINAL mode
+// the WTA of pixel k runs one step behind (after the DP of pixel k+1), so the
+// scheduler can interleave the two dependency chains.
+template <int DIR, int V, int MODE, bool FULL, int PF>
 __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
     const int lane = threadIdx.x;
     const int path = blockIdx.x;
@@ -478,9 +599,9 @@ __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
     cc.init(path, H, W, g.D);
     pc.init(path, H, W, g.D);
 
-    float cb[SWEEP_PF][V], ab[SWEEP_PF][V], sb[SWEEP_PF][V];
+    float cb[PF][V], ab[PF][V], sb[PF][V];
 #pragma unroll
-    for (int u = 0; u < SWEEP_PF; ++u) {
+    for (int u = 0; u < PF; ++u) {
         load_v<V>(cb[u], a.cost + pc.off + e0, active);
         if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
         if (NEED_S) load_v<V>(sb[u], a.s_in + pc.off + e0, active);
@@ -491,9 +612,26 @@ __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
 #pragma unroll
     for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
     float pmin = 0.0f;
+    // FINAL: the previous pixel's total vector and position (WTA deferred)
+    float ptot[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) ptot[v] = SGM_INF;
+    long long ppx = -1;
+
+    auto finish_prev = [&]() {
+        if (ppx >= 0) {
+            int dsp;
+            float f;
+            wta_subpixel<V>(ptot, g.D, a.uniq, dsp, f);
+            if (lane == 0) {
+                a.disp[ppx] = (uint16_t)dsp;
+                a.sub[ppx] = f;
+            }
+        }
+    };
 
     // One DP step on ring slot u; branch-free so the waitcnt pass can keep
-    // exact counts (each slot's loads are waited for SWEEP_PF steps later).
+    // exact counts (each slot's loads are waited for PF steps later).
     auto step = [&](int u, bool refill) {
         float c[V], ai[V], si[V];
 #pragma unroll
@@ -523,18 +661,11 @@ __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
             for (int v = 0; v < V; ++v) o[v] = ai[v] + L[v];
             store_v<V>(a.acc_out + cc.off + e0, o, active);
         } else {
+            finish_prev();
             // cost = ((L1+L2)+L3)+L4 ; cost += ((L5+L6)+L7)+L8  (SGM.cpp:386-390)
-            float tot[V];
 #pragma unroll
-            for (int v = 0; v < V; ++v) tot[v] = si[v] + (ai[v] + L[v]);
-            int dsp;
-            float f;
-            wta_subpixel<V>(tot, lane, g.D, a.uniq, dsp, f);
-            if (lane == 0) {
-                const long long px = (long long)cc.i * W + cc.j;
-                a.disp[px] = (uint16_t)dsp;
-                a.sub[px] = f;
-            }
+            for (int v = 0; v < V; ++v) ptot[v] = si[v] + (ai[v] + L[v]);
+            ppx = (long long)cc.i * W + cc.j;
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) prev[v] = L[v];
@@ -551,26 +682,228 @@ __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
     };
 
     int k0 = 0;
-    for (; k0 + SWEEP_PF <= n; k0 += SWEEP_PF) {
+    for (; k0 + PF <= n; k0 += PF) {
 #pragma unroll
-        for (int u = 0; u < SWEEP_PF; ++u) step(u, true);
+        for (int u = 0; u < PF; ++u) step(u, true);
     }
 #pragma unroll
-    for (int u = 0; u < SWEEP_PF; ++u)
+    for (int u = 0; u < PF; ++u)
         if (k0 + u < n) step(u, false);
+    if (MODE == SWEEP_FINAL) finish_prev();
 }
+
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its
+// global loads (the prefetch ring stays in flight across the barrier).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Partial WTA state over a set of disparities: the minimum m and the first
+// index i holding it, and the smallest value s != m with its first index si
+// (SGM.cpp:383-408: min_cost/min_d, sec_min_cost/sec_min_d).
+struct Wta {
+    float m, s;
+    int i, si;
+};
+
+// Combine two disjoint partial states (ties go to the lower index, so the
+// merge is symmetric and any lane pairing may be used).
+__device__ __forceinline__ Wta wta_merge(const Wta &A, const Wta &B) {
+    Wta r;
+    float c1, c2;
+    int j1, j2;
+    if (A.m < B.m) {
+        r.m = A.m; r.i = A.i; c1 = A.s; j1 = A.si; c2 = B.m; j2 = B.i;
+    } else if (B.m < A.m) {
+        r.m = B.m; r.i = B.i; c1 = B.s; j1 = B.si; c2 = A.m; j2 = A.i;
+    } else {
+        r.m = A.m; r.i = min(A.i, B.i); c1 = A.s; j1 = A.si; c2 = B.s; j2 = B.si;
+    }
+    r.s = fminf(c1, c2);
+    r.si = c1 < c2 ? j1 : (c2 < c1 ? j2 : min(j1, j2));
+    return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ Wta wta_dpp(const Wta &x) {
+    Wta y;
+    y.m = movdppf<CTRL>(x.m);
+    y.s = movdppf<CTRL>(x.s);
+    y.i = movdpp<CTRL>(x.i);
+    y.si = movdpp<CTRL>(x.si);
+    return wta_merge(x, y);
+}
+
+// LDS image of one chunk: PF pixels x D total costs, rows padded by 16 bytes
+// so the consumer's per-pixel reads spread over all banks.
+template <int V>
+constexpr int tbuf_stride() { return 64 * V + 4; }
+
+// The last sweep of a view, fused with the aggregation and the WTA.  Two
+// waves per path: wave 0 runs the DP of direction DIR and forms
+// total = S + (T + L) (SGM.cpp:386-390) for PF pixels at a time into a
+// double-buffered LDS ring; wave 1 runs WTA + uniqueness + sub-pixel
+// (SGM.cpp:376-418, Solver.cpp:577-593) for the previous chunk, all PF pixels
+// at once: 64/PF lanes per pixel, each scanning D*PF/64 costs, merged with
+// DPP.  The DP chain and the WTA then run on two SIMDs in parallel.
+template <int DIR, int V, bool FULL, int PF>
+__global__ __launch_bounds__(128) void sweep_final_kernel(SweepArgs a, Geom g) {
+    constexpr int TS = tbuf_stride<V>();
+    __shared__ __attribute__((aligned(16))) float tbuf[2][PF][TS];
+    __shared__ long long pbuf[2][PF];
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int path = blockIdx.x;
+    const int H = g.H, W = g.W;
+    const long long D = g.D, WD = (long long)g.W * g.D;
+    const int n = DIR < 2 ? W : H;
+    const int nchunks = (n + PF - 1) / PF;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+
+    if (wave == 0) {
+        Cursor<DIR> cc, pc;
+        cc.init(path, H, W, g.D);
+        pc.init(path, H, W, g.D);
+        float cb[PF][V], ab[PF][V], sb[PF][V];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            load_v<V>(cb[u], a.cost + pc.off + e0, active);
+            load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+            load_v<V>(sb[u], a.s_in + pc.off + e0, active);
+            if (pc.k < n - 1) pc.advance(W, D, WD);
+        }
+        float prev[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+        float pmin = 0.0f;
+
+        auto step = [&](int buf, int u, bool refill) {
+            float L[V];
+            dp_step<V>(prev, pmin, cb[u], L, a.p1, a.p2);
+            const bool st = cc.start(W);
+#pragma unroll
+            for (int v = 0; v < V; ++v) L[v] = st ? cb[u][v] : L[v];
+            float lm = L[0];
+#pragma unroll
+            for (int v = 1; v < V; ++v) lm = fminf(lm, L[v]);
+            const float nmin = wave_min(lm);
+            float tot[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) tot[v] = sb[u][v] + (ab[u][v] + L[v]);
+            float *dst = &tbuf[buf][u][e0];
+            if (V == 4) *reinterpret_cast<float4 *>(dst) = make_float4(tot[0], tot[1], tot[2], tot[3]);
+            else if (V == 2) *reinterpret_cast<float2 *>(dst) = make_float2(tot[0], tot[1]);
+            else dst[0] = tot[0];
+            if (lane == 0) pbuf[buf][u] = (long long)cc.i * W + cc.j;
+#pragma unroll
+            for (int v = 0; v < V; ++v) prev[v] = L[v];
+            pmin = nmin;
+            cc.advance(W, D, WD);
+            if (refill) {
+                load_v<V>(cb[u], a.cost + pc.off + e0, active);
+                load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+                load_v<V>(sb[u], a.s_in + pc.off + e0, active);
+                if (pc.k < n - 1) pc.advance(W, D, WD);
+            }
+        };
+        int c = 0;
+        for (; (c + 1) * PF <= n; ++c) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) step(c & 1, u, true);
+            lds_barrier();
+        }
+        if (c < nchunks) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u)
+                if (c * PF + u < n) step(c & 1, u, false);
+            lds_barrier();
+        }
+        lds_barrier();
+    } else {
+        constexpr int LPP = 64 / PF;        // lanes per pixel
+        const int Dn = g.D;
+        const int Q = Dn / LPP;             // disparities per lane (>= 8)
+        const int px = lane / LPP, q = lane - px * LPP;
+        const int d0 = q * Q;
+        lds_barrier();
+        for (int c = 0; c < nchunks; ++c) {
+            const int cnt = min(PF, n - c * PF);
+            const float *row = &tbuf[c & 1][px < cnt ? px : 0][0];
+            // in-lane scan of d0 .. d0+Q-1 in ascending order (SGM.cpp:383-408)
+            Wta w;
+            w.m = SGM_INF; w.s = SGM_INF; w.i = INT_MAX; w.si = INT_MAX;
+            for (int k = 0; k < Q; k += 4) {
+                const float4 x4 = *reinterpret_cast<const float4 *>(row + d0 + k);
+                const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = xs[e];
+                    const int d = d0 + k + e;
+                    if (x < w.m) {
+                        w.s = w.m; w.si = w.i; w.m = x; w.i = d;
+                    } else if (x != w.m && x < w.s) {
+                        w.s = x; w.si = d;
+                    }
+                }
+            }
+            w = wta_dpp<DPP_QP_1032>(w);
+            w = wta_dpp<DPP_QP_2301>(w);
+            if (LPP == 8) w = wta_dpp<DPP_HALF_MIRROR>(w);
+            int d = w.i;
+            if (w.s != SGM_INF && w.m / w.s > a.uniq && abs(w.i - w.si) > 1) d = Dn + 1;
+            float f;
+            if (d > Dn - 1) {
+                f = (float)(Dn + 1);
+            } else if (d == 0 || d == Dn - 1) {
+                f = (float)d;
+            } else {
+                const float av = row[d - 1], bv = row[d + 1], cv = row[d];
+                const float x = d + (av - bv) / (2 * (av + bv - 2 * cv));
+                const float lim = (Dn - 1) * 1.f;
+                f = (lim < x) ? lim : x;  // std::min(x, lim)
+            }
+            if (q == 0 && px < cnt) {
+                const long long pix = pbuf[c & 1][px];
+                a.disp[pix] = (uint16_t)d;
+                a.sub[pix] = f;
+            }
+            lds_barrier();
+        }
+    }
+}
+
+// Steps of loads kept in flight: horizontal paths (few, long, latency-bound)
+// need a deeper ring than the W column/diagonal paths.
+template <int DIR>
+constexpr int sweep_pf() { return DIR < 2 ? 32 : 16; }
 
 template <int DIR, int MODE>
 static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(DIR < 2 ? g.H : g.W);
+    constexpr int PF = sweep_pf<DIR>();
+    if (MODE == SWEEP_FINAL) {
+        if (g.D == 32)
+            sweep_final_kernel<DIR, 1, false, 16><<<grid, 128, 0, st>>>(a, g);
+        else if (g.D == 64)
+            sweep_final_kernel<DIR, 1, true, 16><<<grid, 128, 0, st>>>(a, g);
+        else if (g.D == 128)
+            sweep_final_kernel<DIR, 2, true, 16><<<grid, 128, 0, st>>>(a, g);
+        else
+            sweep_final_kernel<DIR, 4, true, 8><<<grid, 128, 0, st>>>(a, g);
+        return;
+    }
     if (g.D == 32)
-        sweep_kernel<DIR, 1, MODE, false><<<grid, 64, 0, st>>>(a, g);
+        sweep_kernel<DIR, 1, MODE, false, PF><<<grid, 64, 0, st>>>(a, g);
     else if (g.D == 64)
-        sweep_kernel<DIR, 1, MODE, true><<<grid, 64, 0, st>>>(a, g);
+        sweep_kernel<DIR, 1, MODE, true, PF><<<grid, 64, 0, st>>>(a, g);
     else if (g.D == 128)
-        sweep_kernel<DIR, 2, MODE, true><<<grid, 64, 0, st>>>(a, g);
+        sweep_kernel<DIR, 2, MODE, true, PF><<<grid, 64, 0, st>>>(a, g);
     else
-        sweep_kernel<DIR, 4, MODE, true><<<grid, 64, 0, st>>>(a, g);
+        sweep_kernel<DIR, 4, MODE, true, PF / 2><<<grid, 64, 0, st>>>(a, g);
 }
 
 template <int MODE>
