@@ -1,0 +1,361 @@
+// sgm_bodies.h -- per-path role bodies (one wavefront each) shared by the
+// single-role kernels and the multi-role stage kernels (DESIGN.md "Frame
+// schedule": independent roles share one launch so they run concurrently
+// whatever HIP stream -> hardware queue mapping the runtime picks).
+#pragma once
+
+#include "sgm_device.h"
+
+#include <type_traits>
+
+namespace sgm {
+
+template <int V>
+constexpr int pair_k() { return V >= 4 ? 8 : 16; }
+#define K_OF(V) pair_k<V>()
+
+template <int V>
+__device__ __forceinline__ float lane_min(const float (&x)[V]) {
+    float m = x[0];
+#pragma unroll
+    for (int v = 1; v < V; ++v) m = fminf(m, x[v]);
+    return m;
+}
+
+// -------------------------------------------------------- single sweeps
+
+// One direction over one path, one wavefront; lane l holds disparities
+// l*V .. l*V+V-1 (FULL: all 64 lanes hold data, i.e. D >= 64; D = 32 uses
+// lanes 0..31 and +inf above).  Loads run PF steps ahead of the DP through a
+// register ring.  Modes STORE_L / INIT / ACC (the final sweep has its own
+// two-wave kernel).
+template <int DIR, int V, int MODE, bool FULL, int PF>
+__device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, int path) {
+    static_assert(MODE != SWEEP_FINAL, "the final pass is pair_final_kernel");
+    const int lane = threadIdx.x & 63;
+    const int H = g.H, W = g.W;
+    const long long D = g.D, WD = (long long)g.W * g.D;
+    const int n = DIR < 2 ? W : H;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+    constexpr bool NEED_ACC = MODE == SWEEP_ACC;
+
+    Cursor<DIR> cc, pc;
+    cc.init(path, H, W, g.D);
+    pc.init(path, H, W, g.D);
+
+    float cb[PF][V], ab[PF][V];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        load_v<V>(cb[u], a.cost + pc.off + e0, active);
+        if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+        pc.advance_upto(n, W, D, WD);
+    }
+
+    float prev[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+    float pmin = 0.0f;
+
+    // One DP step on ring slot u; branch-free so the waitcnt pass can keep
+    // exact counts (each slot's loads are waited for PF steps later).
+    auto step = [&](int u, bool refill) {
+        float c[V], ai[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            c[v] = cb[u][v];
+            ai[v] = ab[u][v];
+        }
+        float L[V];
+        dp_step<V>(prev, pmin, c, L, a.p1, a.p2);
+        const bool st = cc.start(W);
+#pragma unroll
+        for (int v = 0; v < V; ++v) L[v] = st ? c[v] : L[v];
+        float lm = L[0];
+#pragma unroll
+        for (int v = 1; v < V; ++v) lm = fminf(lm, L[v]);
+        const float nmin = wave_min(lm);
+
+        if constexpr (MODE == SWEEP_STORE_L) {
+            store_v<V>(a.acc_out + cc.off + e0, L, active);
+            if (lane == 0) a.min_out[cc.off / D] = nmin;
+        } else if constexpr (MODE == SWEEP_INIT) {
+            store_v<V>(a.acc_out + cc.off + e0, L, active);
+        } else {
+            float o[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) o[v] = ai[v] + L[v];
+            store_v<V>(a.acc_out + cc.off + e0, o, active);
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = L[v];
+        pmin = nmin;
+        cc.advance(W, D, WD);
+        if (refill) {
+            // refill this ring slot only after its old contents are dead, so
+            // the new load lands in the same registers (no copy, no wait)
+            load_v<V>(cb[u], a.cost + pc.off + e0, active);
+            if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+            pc.advance_upto(n, W, D, WD);
+        }
+    };
+
+    int k0 = 0;
+    for (; k0 + PF <= n; k0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) step(u, true);
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (k0 + u < n) step(u, false);
+}
+
+// --------------------------------------------------------------- pairs
+//
+// Two opposite directions on the same scanlines (L1/L2 rows, L3/L4 columns,
+// L6/L7 wrapped anti-diagonals): the forward body stores its path state every
+// K steps, the backward body recomputes each K-step segment of the forward
+// costs from its checkpoint in registers (each cost is read once for both)
+// and combines  S12 = L1 + L2,  T = (T5 + L6) + L7,  total = ((S12+L3)+L4)+T
+// on the fly in the reference's association order (SGM.cpp:386-390).
+// Segments are counted from the END of a chain of n steps: segment 0 covers
+// [0, r0) with r0 = n - (nseg-1)*K, segment s >= 1 covers [r0+(s-1)K, r0+sK);
+// checkpoint m (m < nseg-1) is the forward state after position r0-1 + mK and
+// seeds segment m+1, so the backward pass meets full segments first.
+
+// ------------------------------------------------------- forward passes
+
+// Forward direction FD (0 = L1, 2 = L3, 5 = L6) over one chain: the DP of
+// SGM.cpp:93-117 with the cost stream prefetched PF steps ahead; the only
+// output is the checkpoint set.
+template <int FD, int V, bool FULL, int PF>
+__device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, int path) {
+    constexpr int K = pair_k<V>();
+    const int lane = threadIdx.x & 63;
+    const int H = g.H, W = g.W;
+    const long long D = g.D, WD = (long long)g.W * g.D;
+    const int n = FD == 0 ? W : H;
+    const int nseg = (n + K - 1) / K;
+    const int r0 = n - (nseg - 1) * K;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+    float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
+    int next_ck = r0 - 1, ck_i = 0;
+
+    Cursor<FD> cc, pc;
+    cc.init(path, H, W, g.D);
+    pc.init(path, H, W, g.D);
+    float cb[PF][V];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        load_v<V>(cb[u], a.cost + pc.off + e0, active);
+        pc.advance_upto(n, W, D, WD);
+    }
+    float prev[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+    float pmin = 0.0f;
+
+    auto step = [&](int u, bool refill) {
+        float L[V];
+        dp_step<V>(prev, pmin, cb[u], L, a.p1, a.p2);
+        const bool st = cc.start(W);
+#pragma unroll
+        for (int v = 0; v < V; ++v) L[v] = st ? cb[u][v] : L[v];
+        const float nmin = wave_min(lane_min(L));
+        if (cc.k == next_ck && ck_i < nseg - 1) {
+            store_v<V>(ck + (size_t)ck_i * g.D, L, active);
+            ++ck_i;
+            next_ck += K;
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = L[v];
+        pmin = nmin;
+        cc.advance(W, D, WD);
+        if (refill) {
+            load_v<V>(cb[u], a.cost + pc.off + e0, active);
+            pc.advance_upto(n, W, D, WD);
+        }
+    };
+    int k0 = 0;
+    for (; k0 + PF <= n; k0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) step(u, true);
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (k0 + u < n) step(u, false);
+}
+
+// ------------------------------------------------------- backward pass
+
+// tb/pb: the FINAL mode's LDS ring (two chunks of K total-cost rows and
+// pixel positions), unused otherwise.
+template <int FAM, int V, bool FULL, int MODE>
+__device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, int path,
+                                              float (*tb)[K_OF(V)][tbuf_stride<V>()],
+                                              long long (*pb)[K_OF(V)]) {
+    constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
+    constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
+    constexpr int K = pair_k<V>();
+    constexpr bool FINAL = MODE == PAIR_FINAL;
+    constexpr bool NEED_ACC = MODE != PAIR_INIT2;
+    constexpr bool NEED_S = FINAL;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int H = g.H, W = g.W;
+    const long long D = g.D, WD = (long long)g.W * g.D;
+    const int n = FAM == PAIR_H ? W : H;
+    const int nseg = (n + K - 1) / K;
+    const int r0 = n - (nseg - 1) * K;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+
+    if constexpr (FINAL) {
+        if (wave == 1) {  // WTA consumer, one chunk per segment
+            lds_barrier();
+            for (int c = 0; c < nseg; ++c) {
+                wta_consume_chunk<V, K>(tb[c & 1], pb[c & 1], c == nseg - 1 ? r0 : K, lane,
+                                        g.D, a.uniq, a.disp, a.sub);
+                lds_barrier();
+            }
+            return;
+        }
+    }
+
+    // the backward direction walks the same chain in reverse: for the wrapped
+    // anti-diagonals chain g of L6 is chain (g - (H-1)) mod W of L7
+    const int bpath = FAM == PAIR_D2 ? uniform(((path - (H - 1)) % W + W) % W) : path;
+    const float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
+
+    Cursor<BD> bc, pc;
+    bc.init(bpath, H, W, g.D);
+    pc.init(bpath, H, W, g.D);
+    float ab[K][V], sb[K][V];
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+        if (NEED_S) load_v<V>(sb[u], a.s_in + pc.off + e0, active);
+        pc.advance_upto(n, W, D, WD);
+    }
+
+    float c0[K][V], c1[K][V], lf[K][V];
+    float prevb[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
+    float pminb = 0.0f;
+
+    // costs of segment s into cs; array slot kk holds position
+    // pos0 + kk - (K - cnt) (slots below K - cnt are unused for the partial
+    // segment and load position pos0 again)
+    auto load_seg = [&](float (&cs)[K][V], int s) {
+        const int cnt = s == 0 ? r0 : K;
+        const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
+        Cursor<FD> fc;
+        fc.init_at(path, pos0, H, W, g.D);
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) {
+            load_v<V>(cs[kk], a.cost + fc.off + e0, active);
+            fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
+        }
+    };
+
+    auto process_seg = [&](float (&cs)[K][V], int s, auto full_tag) {
+        constexpr bool FULLSEG = decltype(full_tag)::value;
+        const int cnt = FULLSEG ? K : (s == 0 ? r0 : K);
+        const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
+        const int skip = K - cnt;
+        // 1) recompute the forward costs of this segment from its checkpoint
+        float pf[V];
+        float pminf = 0.0f;
+        if (s > 0) {
+            load_v<V>(pf, ck + (size_t)(s - 1) * g.D, active);
+            pminf = wave_min(lane_min(pf));
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v) pf[v] = SGM_INF;
+        }
+        Cursor<FD> fc;
+        fc.init_at(path, pos0, H, W, g.D);
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) {
+            if (FULLSEG || kk >= skip) {
+                float L[V];
+                dp_step<V>(pf, pminf, cs[kk], L, a.p1, a.p2);
+                const bool st = fc.start(W);
+#pragma unroll
+                for (int v = 0; v < V; ++v) L[v] = st ? cs[kk][v] : L[v];
+                pminf = wave_min(lane_min(L));
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    lf[kk][v] = L[v];
+                    pf[v] = L[v];
+                }
+                fc.advance(W, D, WD);
+            }
+        }
+        // 2) backward direction over the segment, combined on the fly
+        const int buf = (nseg - 1 - s) & 1;
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const int kk = K - 1 - r;
+            if (FULLSEG || kk >= skip) {
+                float L[V];
+                dp_step<V>(prevb, pminb, cs[kk], L, a.p1, a.p2);
+                const bool st = bc.start(W);
+#pragma unroll
+                for (int v = 0; v < V; ++v) L[v] = st ? cs[kk][v] : L[v];
+                const float nmin = wave_min(lane_min(L));
+                if constexpr (MODE == PAIR_INIT2) {
+                    float o[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v) o[v] = lf[kk][v] + L[v];
+                    store_v<V>(a.out + bc.off + e0, o, active);
+                } else if constexpr (MODE == PAIR_ACC) {
+                    float o[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v) o[v] = (ab[r][v] + lf[kk][v]) + L[v];
+                    store_v<V>(a.out + bc.off + e0, o, active);
+                } else if constexpr (FINAL) {
+                    float tot[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v) tot[v] = ((sb[r][v] + lf[kk][v]) + L[v]) + ab[r][v];
+                    store_lds_v<V>(&tb[buf][r][e0], tot);
+                    if (lane == 0) pb[buf][r] = (long long)bc.i * W + bc.j;
+                }
+#pragma unroll
+                for (int v = 0; v < V; ++v) prevb[v] = L[v];
+                pminb = nmin;
+                bc.advance(W, D, WD);
+                if (NEED_ACC) load_v<V>(ab[r], a.acc_in + pc.off + e0, active);
+                if (NEED_S) load_v<V>(sb[r], a.s_in + pc.off + e0, active);
+                pc.advance_upto(n, W, D, WD);
+            }
+        }
+        if (FINAL) lds_barrier();
+    };
+
+    // Full segments two at a time (branch-free bodies keep the wait counts
+    // exact, so each segment's cost loads stay in flight during the previous
+    // segment), then segment 0, which may be partial.
+    using full_t = std::integral_constant<bool, true>;
+    using part_t = std::integral_constant<bool, false>;
+    load_seg(c0, nseg - 1);
+    int s = nseg - 1;
+    for (; s >= 2; s -= 2) {
+        load_seg(c1, s - 1);
+        process_seg(c0, s, full_t{});
+        load_seg(c0, s - 2);
+        process_seg(c1, s - 1, full_t{});
+    }
+    if (s == 1) {
+        load_seg(c1, 0);
+        process_seg(c0, 1, full_t{});
+        process_seg(c1, 0, part_t{});
+    } else {
+        process_seg(c0, 0, part_t{});
+    }
+    if (FINAL) lds_barrier();
+}
+
+}  // namespace sgm

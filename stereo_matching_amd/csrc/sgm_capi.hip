@@ -1,13 +1,15 @@
 // sgm_capi.hip -- the C-ABI of libsgm_hip.so (include/sgm_hip.h).
 //
-// Host orchestration of one frame (DESIGN.md "Frame schedule"):
+// Host orchestration of one view (DESIGN.md "Frame schedule"), 73.5 B of HBM
+// traffic per pixel-disparity, six launches on one stream:
 //
-//   caller stream : census L,R -> cost_h(L) -> cost_v(L) -> L1 L2 L3 L4 (S_L) --.
-//   aux0          :                      \-> L5 L6 L7 (T_L) -------------------+-> L8 FINAL(L)
-//   aux1          : cost_h(R) -> cost_v(R) -> L1 L2 L3 L4 (S_R) --.            |
-//   aux2          :                     \-> L5 L6 L7 (T_R) -------+-> L8 FINAL(R)
-//   caller stream : join -> LR check
+//   census L,R -> cost_h -> vfwd (vertical IIR + L3 checkpoints)
+//   -> stage A (L1 fwd | L5 | L6 fwd) -> stage B (L2 bwd | L7 bwd) -> L8
+//   -> final (L4 bwd recomputing L3, sum, WTA, sub-pixel)
 //
+// Concurrency between independent roles comes from sharing a launch (stage
+// A/B), not from streams (the runtime may map streams onto one hardware
+// queue).  The right view runs on a second stream; then the LR check.
 // All device memory is allocated at sgm_create (the reference allocates its
 // scratch in the constructors, Solver.cpp:18-27 and SGM.cpp:7-24).
 #include "../../include/sgm_hip.h"
@@ -32,8 +34,8 @@ struct sgm_handle {
     int serialize;        // SGM_SERIALIZE=1: every kernel on one stream (isolated timings)
     size_t bytes;
     hipStream_t st;       // the handle's own stream (host API, stages)
-    hipStream_t aux[3];
-    hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_v1;
+    hipStream_t aux[1];      // right view (two-view frames)
+    hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1;
     uint8_t *d_in[2];     // full-size input staging (host API)
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
@@ -44,6 +46,7 @@ struct sgm_handle {
     float *d_sub[2];      // sub-pixel disparity
     float *d_out;         // LR-checked output (host API)
     float *d_min;         // minL (stage_path)
+    float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
     char err[512];
     // profiling (sgm_set_profiling)
     int profiling;
@@ -122,9 +125,12 @@ void free_all(sgm_handle *h) {
     }
     (void)hipFree(h->d_out);
     (void)hipFree(h->d_min);
+    for (auto &v : h->d_ck)
+        for (auto p : v) (void)hipFree(p);
     if (h->st) (void)hipStreamDestroy(h->st);
     for (auto &s : h->aux) if (s) (void)hipStreamDestroy(s);
-    hipEvent_t evs[] = {h->ev_ct, h->ev_c[0], h->ev_c[1], h->ev_t[0], h->ev_t[1], h->ev_v1};
+    hipEvent_t evs[] = {h->ev_ct, h->ev_c[0], h->ev_c[1], h->ev_t[0], h->ev_t[1],
+                        h->ev_s[0], h->ev_s[1], h->ev_v1};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -184,49 +190,86 @@ SweepArgs sweep_args(const sgm_handle *h) {
     return a;
 }
 
-// The 8-path aggregation of one view: S chain (L1..L4) on `s_st`, T chain
-// (L5..L7) on `t_st`, then L8 fused with the sum, WTA, uniqueness and
-// sub-pixel on `s_st`.  t buffer may alias the (dead) horizontally filtered
-// cost volume.
-int aggregate_view(sgm_handle *h, const float *cost, float *S, float *T, uint16_t *disp, float *sub,
-                   hipStream_t s_st, hipStream_t t_st, hipEvent_t ev_src, hipEvent_t ev_t) {
-    SweepArgs a = sweep_args(h);
-    a.cost = cost;
-    HIPCHK(h, hipStreamWaitEvent(t_st, ev_src, 0));
-    // T chain: T = ((L5 + L6) + L7)
-    a.acc_out = T;
-    HIPCHK(h, sweep(h, SGM_DIR_L5, sgm::SWEEP_INIT, a, t_st));
-    a.acc_in = T;
-    HIPCHK(h, sweep(h, SGM_DIR_L6, sgm::SWEEP_ACC, a, t_st));
-    HIPCHK(h, sweep(h, SGM_DIR_L7, sgm::SWEEP_ACC, a, t_st));
-    HIPCHK(h, hipEventRecord(ev_t, t_st));
-    // S chain: S = ((L1 + L2) + L3) + L4
-    a.acc_in = nullptr;
-    a.acc_out = S;
-    HIPCHK(h, sweep(h, SGM_DIR_L1, sgm::SWEEP_INIT, a, s_st));
-    a.acc_in = S;
-    HIPCHK(h, sweep(h, SGM_DIR_L2, sgm::SWEEP_ACC, a, s_st));
-    HIPCHK(h, sweep(h, SGM_DIR_L3, sgm::SWEEP_ACC, a, s_st));
-    HIPCHK(h, sweep(h, SGM_DIR_L4, sgm::SWEEP_ACC, a, s_st));
-    // join, then total = S + (T + L8) -> WTA -> sub-pixel
-    HIPCHK(h, hipStreamWaitEvent(s_st, ev_t, 0));
-    a.acc_in = T;
-    a.s_in = S;
-    a.acc_out = nullptr;
-    a.disp = disp;
-    a.sub = sub;
-    HIPCHK(h, sweep(h, SGM_DIR_L8, sgm::SWEEP_FINAL, a, s_st));
+sgm::PairArgs pair_args(const sgm_handle *h) {
+    sgm::PairArgs a{};
+    a.p1 = (float)h->p.p1;
+    a.p2 = (float)h->p.p2;
+    a.uniq = h->p.uniqueness;
+    return a;
+}
+
+hipError_t pair_fwd(sgm_handle *h, int fam, const sgm::PairArgs &a, hipStream_t st) {
+    static const char *names[3] = {"pair_fwd_L1", "pair_fwd_L3", "pair_fwd_L6"};
+    const double elems = (double)h->g.H * h->g.W * h->g.D;
+    return timed(h, names[fam], elems, st, [&] { return sgm::launch_pair_fwd(fam, a, h->g, st); });
+}
+
+hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hipStream_t st) {
+    static const char *names[3] = {"pair_bwd_L2_init2", "pair_bwd_L4_final", "pair_bwd_L7_acc"};
+    const double elems = (double)h->g.H * h->g.W * h->g.D;
+    return timed(h, names[fam], elems, st,
+                 [&] { return sgm::launch_pair_bwd(fam, mode, a, h->g, st); });
+}
+
+// The 8-path aggregation of one view, given the final cost volume and the L3
+// checkpoints (written by vfwd, or by the PAIR_V forward pass here when
+// `need_v_ckpt`), as three launches on one stream:
+//   stage A: L1 fwd (ckpt) | L5 -> T5 | L6 fwd (ckpt)
+//   stage B: L2 bwd: S12 = L1 + L2 | L7 bwd: T = (T5 + L6) + L7
+//   L8:      T += L8
+//   final:   L4 bwd recomputing L3: total = ((S12 + L3) + L4) + T -> WTA
+// (the reference's order, SGM.cpp:386-390).  T may alias the dead
+// horizontally filtered volume.
+int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *T, uint16_t *disp,
+                   float *sub, hipStream_t st, bool need_v_ckpt) {
+    float **ck = h->d_ck[view];
+    const double elems = (double)h->g.H * h->g.W * h->g.D;
+    sgm::PairArgs pa = pair_args(h);
+    pa.cost = cost;
+    if (need_v_ckpt) {
+        pa.ckpt = ck[sgm::PAIR_V];
+        HIPCHK(h, pair_fwd(h, sgm::PAIR_V, pa, st));
+    }
+    sgm::PairArgs h1 = pa, d6 = pa;
+    h1.ckpt = ck[sgm::PAIR_H];
+    d6.ckpt = ck[sgm::PAIR_D2];
+    SweepArgs l5 = sweep_args(h);
+    l5.cost = cost;
+    l5.acc_out = T;
+    HIPCHK(h, timed(h, "stage_a", elems, st,
+                    [&] { return sgm::launch_stage_a(h1, l5, d6, h->g, st); }));
+    sgm::PairArgs h2 = h1, d7 = d6;
+    h2.out = S;
+    d7.acc_in = T;
+    d7.out = T;
+    HIPCHK(h, timed(h, "stage_b", elems, st,
+                    [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
+    SweepArgs l8 = sweep_args(h);
+    l8.cost = cost;
+    l8.acc_in = T;
+    l8.acc_out = T;
+    HIPCHK(h, sweep(h, SGM_DIR_L8, sgm::SWEEP_ACC, l8, st));
+    pa.ckpt = ck[sgm::PAIR_V];
+    pa.s_in = S;
+    pa.acc_in = T;
+    pa.disp = disp;
+    pa.sub = sub;
+    HIPCHK(h, pair_bwd(h, sgm::PAIR_V, sgm::PAIR_FINAL, pa, st));
     return SGM_OK;
 }
 
+// build_dsi_from_table[_beta] + horizontal IIR (cost_h), then the vertical IIR
+// fused with the L3 forward pass (vfwd).
 int cost_view(sgm_handle *h, int view, const uint8_t *sky, int sky_pitch, hipStream_t st) {
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     HIPCHK(h, timed(h, "cost_h", elems, st, [&] {
                return sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky, sky_pitch, view, 1, h->g,
                                          h->d_ch[view], st);
            }));
-    HIPCHK(h, timed(h, "cost_v", elems, st, [&] {
-               return sgm::launch_cost_v(h->d_ch[view], h->d_c[view], 1, h->g, st);
+    sgm::PairArgs pa = pair_args(h);
+    pa.ckpt = h->d_ck[view][sgm::PAIR_V];
+    HIPCHK(h, timed(h, "vfwd", elems, st, [&] {
+               return sgm::launch_vfwd(h->d_ch[view], h->d_c[view], pa, h->g, st);
            }));
     return SGM_OK;
 }
@@ -236,9 +279,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
     const Geom g = h->g;
     int rc;
-    hipStream_t aux0 = h->serialize ? st : h->aux[0];
-    hipStream_t aux1 = h->serialize ? st : h->aux[1];
-    hipStream_t aux2 = h->serialize ? st : h->aux[2];
+    hipStream_t aux1 = h->serialize ? st : h->aux[0];  // right view
     const double npx = (double)g.H * g.W;
     HIPCHK(h, timed(h, "census", npx, st, [&] {
                return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st);
@@ -254,12 +295,12 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     }
     if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
     HIPCHK(h, hipEventRecord(h->ev_c[0], st));
-    if ((rc = aggregate_view(h, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
-                             aux0, h->ev_c[0], h->ev_t[0])) != SGM_OK)
+    if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
+                             false)) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
-        if ((rc = aggregate_view(h, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
-                                 aux1, aux2, h->ev_c[1], h->ev_t[1])) != SGM_OK)
+        if ((rc = aggregate_view(h, 1, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
+                                 aux1, false)) != SGM_OK)
             return rc;
         HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
         HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
@@ -345,7 +386,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         for (auto &s : h->aux)
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
         if (rc) break;
-        hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1], &h->ev_v1};
+        hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1],
+                             &h->ev_s[0], &h->ev_s[1], &h->ev_v1};
         for (auto e : evs)
             if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { rc = SGM_ERR_HIP; break; }
         if (rc) break;
@@ -360,6 +402,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if ((rc = dalloc(h, &h->d_s[v], nvol))) break;
             if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
             if ((rc = dalloc(h, &h->d_sub[v], npx))) break;
+            for (int f = 0; f < 3 && !rc; ++f)
+                rc = dalloc(h, &h->d_ck[v][f], sgm::pair_ckpt_floats(f, h->g));
         }
         if (!rc && h->nviews == 1) {  // stage_lr needs a second sub-pixel map
             rc = dalloc(h, &h->d_sub[1], npx);
@@ -550,7 +594,13 @@ int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr, cons
     if (sky) HIPCHK(h, hipMemcpyAsync(h->d_sky[0], sky, npx, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky ? h->d_sky[0] : nullptr, h->g.W, view,
                                  filters & 1, h->g, h->d_ch[0], h->st));
-    HIPCHK(h, sgm::launch_cost_v(h->d_ch[0], h->d_c[0], filters & 2, h->g, h->st));
+    if (filters & 2) {
+        sgm::PairArgs pa = pair_args(h);
+        pa.ckpt = h->d_ck[0][sgm::PAIR_V];
+        HIPCHK(h, sgm::launch_vfwd(h->d_ch[0], h->d_c[0], pa, h->g, h->st));
+    } else {
+        HIPCHK(h, sgm::launch_copy(h->d_ch[0], h->d_c[0], h->g, h->st));
+    }
     HIPCHK(h, hipMemcpyAsync(cost, h->d_c[0], nvol * 4, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return SGM_OK;
@@ -578,8 +628,8 @@ int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float 
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, hipEventRecord(h->ev_c[0], h->st));
-    int rc = aggregate_view(h, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], h->st,
-                            h->aux[0], h->ev_c[0], h->ev_t[0]);
+    int rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0],
+                            h->st, true);
     if (rc) return rc;
     if (disp) HIPCHK(h, hipMemcpyAsync(disp, h->d_disp[0], npx * 2, hipMemcpyDeviceToHost, h->st));
     if (sub) HIPCHK(h, hipMemcpyAsync(sub, h->d_sub[0], npx * 4, hipMemcpyDeviceToHost, h->st));

@@ -1,0 +1,288 @@
+// sgm_cost.hip -- census, DSI + horizontal IIR, vertical IIR.
+// CDNA4 (gfx950) kernels of the semi-global matcher.
+//
+// Stage map (reference -> kernel), full design in DESIGN.md:
+//   cv::GaussianBlur + CT_pts     Solver.cpp:120-140, cost.cpp:99-129  -> census_kernel
+//   build_dsi_from_table[_beta]   Solver.cpp:143-248
+//     + cost_horizontal_filter    Solver.cpp:296-330                   -> cost_h_kernel
+//   cost_vertical_filter          Solver.cpp:333-368                   -> cost_v_kernel
+//   L1..L8 path DP                SGM.cpp:81-369                       -> sweep_kernel<DIR,..>
+//   aggregation + WTA + unique    SGM.cpp:372-418
+//     + compute_subpixel          Solver.cpp:569-597                   -> sweep_kernel<..,FINAL>
+//   LR check                      SGM.cpp:803-818                      -> lr_kernel
+//
+// Bit-exactness rules (DESIGN.md "Numerics"): built with -ffp-contract=off,
+// no fast-math, correctly rounded f32 division; every float expression keeps
+// the reference's association order.
+#include "sgm_device.h"
+
+namespace sgm {
+
+// ---------------------------------------------------------------- census
+
+// Pinned cv::GaussianBlur(Size(3,3), 2, 1) on CV_8U (Solver.cpp:124-125):
+// OpenCV 3.x fixed-point separable filter, kernels {82,93,82} x {70,116,70},
+// BORDER_REFLECT_101, (acc + 2^15) >> 16, saturated.  Same formula as
+// oracle/sgm_oracle.c:orc_blur (parity unpinned at this boundary).
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * n - 2 - i : i;
+}
+
+__device__ __forceinline__ int blur_at(const uint8_t *src, int pitch, int step, int H, int W,
+                                       int y, int x) {
+    const int xm = reflect101(x - 1, W) * step, x0 = x * step, xp = reflect101(x + 1, W) * step;
+    const int ys[3] = {reflect101(y - 1, H), y, reflect101(y + 1, H)};
+    const int ky[3] = {70, 116, 70};
+    int acc = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const uint8_t *row = src + (size_t)ys[r] * step * pitch;
+        acc += ky[r] * (82 * row[xm] + 93 * row[x0] + 82 * row[xp]);
+    }
+    const int v = (acc + (1 << 15)) >> 16;
+    return v > 255 ? 255 : v;
+}
+
+constexpr int CT_TW = 64, CT_TH = 8;
+
+// CT_pts (cost.cpp:99-129) for one image; window (7/s) x (9/s), MSB first,
+// centre skipped, coordinates clamped to the (working-grid) edge.  The
+// (blurred) window is staged in LDS at clamped coordinates.
+template <int HH, int HWW>
+__global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__ src, int pitch,
+                                                     int step, int H, int W, int blur,
+                                                     uint64_t *__restrict__ ct) {
+    constexpr int TR = CT_TH + 2 * HH, TC = CT_TW + 2 * HWW;
+    __shared__ uint8_t tile[TR][TC];
+    const int x0 = blockIdx.x * CT_TW, y0 = blockIdx.y * CT_TH;
+    for (int idx = threadIdx.x; idx < TR * TC; idx += 256) {
+        const int ty = idx / TC, tx = idx - ty * TC;
+        const int y = clampi(y0 + ty - HH, 0, H - 1), x = clampi(x0 + tx - HWW, 0, W - 1);
+        tile[ty][tx] = blur ? (uint8_t)blur_at(src, pitch, step, H, W, y, x)
+                            : src[(size_t)y * step * pitch + (size_t)x * step];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 63;
+    for (int r = threadIdx.x >> 6; r < CT_TH; r += 4) {
+        const int y = y0 + r, x = x0 + tx;
+        if (y >= H || x >= W) continue;
+        const uint8_t c = tile[r + HH][tx + HWW];
+        uint64_t v = 0;
+#pragma unroll
+        for (int di = -HH; di <= HH; ++di)
+#pragma unroll
+            for (int dj = -HWW; dj <= HWW; ++dj) {
+                if (di == 0 && dj == 0) continue;
+                v = (v << 1) | (uint64_t)(tile[r + HH + di][tx + HWW + dj] > c);
+            }
+        ct[(size_t)y * W + x] = v;
+    }
+}
+
+hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64_t *ct,
+                         hipStream_t st) {
+    dim3 grid((g.W + CT_TW - 1) / CT_TW, (g.H + CT_TH - 1) / CT_TH);
+    if (g.scale == 1)
+        census_kernel<3, 4><<<grid, 256, 0, st>>>(src, pitch, 1, g.H, g.W, blur, ct);
+    else
+        census_kernel<1, 2><<<grid, 256, 0, st>>>(src, pitch, 2, g.H, g.W, blur, ct);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------ DSI + horizontal IIR
+
+// One thread per (row, d) chain, R rows per block (R*D threads).  The census
+// rows of both images (and the sky row) are staged in LDS once per block; the
+// raw Hamming DSI (Solver.cpp:143-248, sky override :165-178) is produced on
+// the fly and fed straight into the in-place horizontal IIR of
+// Solver.cpp:296-330, restated with a register history: with h = WIN/2 and
+// LAG = WIN-h-1 the reference writes position LAG+t at step t, adds raw[WIN+t]
+// and subtracts the value at position t, which is the step-(t-LAG) output once
+// t >= LAG and raw before.
+constexpr int COSTH_MAX_LDS = 64 * 1024;
+
+template <int VIEW, int WIN, bool SKY, bool FILTER>
+__global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
+                                                     const uint64_t *__restrict__ ctr,
+                                                     const uint8_t *__restrict__ sky,
+                                                     int sky_pitch, int H, int W, int D, int scale,
+                                                     int R, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
+    uint64_t *sr = sl + (size_t)R * W;
+    uint8_t *ss = reinterpret_cast<uint8_t *>(sr + (size_t)R * W);
+    const int row0 = blockIdx.x * R;
+    for (int idx = threadIdx.x; idx < R * W; idx += blockDim.x) {
+        const int r = idx / W, j = idx - r * W, i = row0 + r;
+        if (i < H) {
+            sl[idx] = ctl[(size_t)i * W + j];
+            sr[idx] = ctr[(size_t)i * W + j];
+            if (SKY) ss[idx] = sky[(size_t)i * sky_pitch + j];
+        }
+    }
+    __syncthreads();
+    const int r = threadIdx.x / D, d = threadIdx.x - r * D;
+    const int i = row0 + r;
+    if (i >= H) return;
+    const uint64_t *cl = sl + (size_t)r * W;
+    const uint64_t *cr = sr + (size_t)r * W;
+    const uint8_t *sk = ss + (size_t)r * W;
+    const int ds = d / scale;
+    float *o = out + (size_t)i * W * D + d;
+
+    auto raw = [&](int j) -> float {
+        uint64_t a, b;
+        if (VIEW == 0) {
+            a = cl[j];
+            b = cr[max(j - ds, 0)];
+        } else {
+            a = cl[min(j + ds, W - 1)];
+            b = cr[j];
+        }
+        const float c = (float)__popcll(a ^ b);
+        if (SKY && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
+        return c;
+    };
+
+    if (!FILTER) {
+        for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
+        return;
+    }
+    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1;
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < WIN; ++k) sum += raw(k);
+#pragma unroll
+    for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
+    const int T = W - 2 * HALF;
+    float o1 = 0.0f, o2 = 0.0f;
+    const float r0 = raw(0), r1 = raw(1);
+#pragma unroll 8
+    for (int t = 0; t < T; ++t) {
+        const float v = div_win<WIN>(sum);
+        o[(size_t)(LAG + t) * D] = v;
+        if (t == T - 1) break;
+        sum += raw(WIN + t);
+        float a;
+        if (LAG == 0) a = v;
+        else if (LAG == 1) a = t >= 1 ? o1 : r0;
+        else a = t >= 2 ? o2 : (t == 0 ? r0 : r1);
+        sum -= a;
+        o2 = o1;
+        o1 = v;
+    }
+    for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
+}
+
+// Fallback for rows too wide to stage in LDS (W*16 B > 64 KiB): census words
+// read straight from global memory.
+template <int VIEW, int WIN, bool SKY, bool FILTER>
+__global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__restrict__ ctl,
+                                                            const uint64_t *__restrict__ ctr,
+                                                            const uint8_t *__restrict__ sky,
+                                                            int sky_pitch, int H, int W, int D,
+                                                            int scale, float *__restrict__ out) {
+    const int rows_per_block = 256 / D;
+    const int r = threadIdx.x / D, d = threadIdx.x - r * D;
+    const int i = blockIdx.x * rows_per_block + r;
+    if (i >= H) return;
+    const uint64_t *cl = ctl + (size_t)i * W;
+    const uint64_t *cr = ctr + (size_t)i * W;
+    const uint8_t *sk = SKY ? sky + (size_t)i * sky_pitch : nullptr;
+    const int ds = d / scale;
+    float *o = out + (size_t)i * W * D + d;
+    auto raw = [&](int j) -> float {
+        if (SKY && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
+        const uint64_t a = VIEW == 0 ? cl[j] : cl[min(j + ds, W - 1)];
+        const uint64_t b = VIEW == 0 ? cr[max(j - ds, 0)] : cr[j];
+        return (float)__popcll(a ^ b);
+    };
+    if (!FILTER) {
+        for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
+        return;
+    }
+    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1;
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < WIN; ++k) sum += raw(k);
+#pragma unroll
+    for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
+    const int T = W - 2 * HALF;
+    float o1 = 0.0f, o2 = 0.0f;
+    for (int t = 0; t < T; ++t) {
+        const float v = div_win<WIN>(sum);
+        o[(size_t)(LAG + t) * D] = v;
+        if (t == T - 1) break;
+        sum += raw(WIN + t);
+        float a;
+        if (LAG == 0) a = v;
+        else if (LAG == 1) a = t >= 1 ? o1 : raw(t);
+        else a = t >= 2 ? o2 : raw(t);
+        sum -= a;
+        o2 = o1;
+        o1 = v;
+    }
+    for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
+}
+
+template <int VIEW, int WIN, bool SKY, bool FILTER>
+static void launch_cost_h_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+                            int sky_pitch, Geom g, float *out, hipStream_t st) {
+    const size_t row_bytes = (size_t)g.W * (16 + (SKY ? 1 : 0));
+    int R = (int)(COSTH_MAX_LDS / row_bytes);
+    if (R > 256 / g.D) R = 256 / g.D;
+    if (R >= 1) {
+        const size_t smem = (size_t)R * row_bytes;
+        cost_h_kernel<VIEW, WIN, SKY, FILTER><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+            ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
+    } else {
+        const int rpb = 256 / g.D;
+        cost_h_global_kernel<VIEW, WIN, SKY, FILTER><<<dim3((g.H + rpb - 1) / rpb), 256, 0, st>>>(
+            ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, out);
+    }
+}
+
+template <int VIEW, int WIN>
+static void launch_cost_h_w(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+                            int sky_pitch, int filter, Geom g, float *out, hipStream_t st) {
+    if (sky) {
+        if (filter) launch_cost_h_t<VIEW, WIN, true, true>(ctl, ctr, sky, sky_pitch, g, out, st);
+        else launch_cost_h_t<VIEW, WIN, true, false>(ctl, ctr, sky, sky_pitch, g, out, st);
+    } else {
+        if (filter) launch_cost_h_t<VIEW, WIN, false, true>(ctl, ctr, sky, sky_pitch, g, out, st);
+        else launch_cost_h_t<VIEW, WIN, false, false>(ctl, ctr, sky, sky_pitch, g, out, st);
+    }
+}
+
+hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
+                         int sky_pitch, int view, int filter, Geom g, float *out,
+                         hipStream_t st) {
+    if (view == 0) {
+        if (g.scale == 1) launch_cost_h_w<0, 5>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
+        else launch_cost_h_w<0, 2>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
+    } else {
+        if (g.scale == 1) launch_cost_h_w<1, 5>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
+        else launch_cost_h_w<1, 2>(ctl, ctr, sky, sky_pitch, filter, g, out, st);
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------ vertical pass
+
+// The vertical IIR (Solver.cpp:333-368) runs fused with the L3 forward pass in
+// sgm_pair.hip (vfwd_kernel); without the filter the volume is copied.
+__global__ __launch_bounds__(256) void copy_kernel(const float *__restrict__ in,
+                                                   float *__restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st) {
+    const size_t n = (size_t)g.W * g.D * g.H;
+    copy_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>(in, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace sgm

@@ -1,0 +1,407 @@
+// sgm_device.h -- device-side building blocks shared by the gfx950 kernels:
+// DPP / permlane wave reductions, path cursors, the DP step of SGM.cpp:93-117
+// and the WTA of SGM.cpp:376-418 + Solver.cpp:577-593.
+#pragma once
+
+#include "sgm_internal.h"
+
+#include <float.h>
+#include <limits.h>
+
+namespace sgm {
+
+#define SGM_INF __builtin_inff()
+
+// ---------------------------------------------------------------- helpers
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// DPP move with an explicit fill value for lanes whose source is invalid or
+// masked off (bound_ctrl = 0 keeps `old`).
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ float dppf(float old, float src) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src),
+                                                      CTRL, ROW_MASK, BANK_MASK, false));
+}
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ int dppi(int old, int src) {
+    return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false);
+}
+
+// DPP controls (GFX9 encoding, valid on gfx950).
+constexpr int DPP_QP_1032 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int DPP_QP_2301 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141;
+constexpr int DPP_MIRROR = 0x140;
+constexpr int DPP_BCAST15 = 0x142;
+constexpr int DPP_BCAST31 = 0x143;
+constexpr int DPP_WAVE_SHL1 = 0x130;  // lane i reads lane i+1
+constexpr int DPP_WAVE_SHR1 = 0x138;  // lane i reads lane i-1
+
+// Plain DPP move (no fill value, bound_ctrl set): only for patterns whose
+// consumed lanes all have a valid source, so the compiler folds the move into
+// the consuming VALU op (v_min_f32_dpp).
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ int movdpp(int src) {
+    return __builtin_amdgcn_mov_dpp(src, CTRL, ROW_MASK, BANK_MASK, true);
+}
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ float movdppf(float src) {
+    return __int_as_float(movdpp<CTRL, ROW_MASK, BANK_MASK>(__float_as_int(src)));
+}
+
+// Minimum over the 64 lanes, left in EVERY lane (a VGPR, no readlane on the
+// DP chain): the quad, half-row and row mirrors give each lane its row (16
+// lane) minimum; v_permlane16_swap pairs rows 0<->1 and 2<->3, and
+// v_permlane32_swap the two wave halves (gfx950).
+__device__ __forceinline__ float wave_min(float x) {
+    x = fminf(x, movdppf<DPP_QP_1032>(x));
+    x = fminf(x, movdppf<DPP_QP_2301>(x));
+    x = fminf(x, movdppf<DPP_HALF_MIRROR>(x));
+    x = fminf(x, movdppf<DPP_MIRROR>(x));
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x),
+                                                    false, false);
+    x = fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x),
+                                                    false, false);
+    return fminf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
+// Same, returned as a wave-uniform scalar.
+__device__ __forceinline__ float wave_min_u(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_min(x))));
+}
+
+__device__ __forceinline__ int wave_min_i(int x) {
+    x = min(x, movdpp<DPP_QP_1032>(x));
+    x = min(x, movdpp<DPP_QP_2301>(x));
+    x = min(x, movdpp<DPP_HALF_MIRROR>(x));
+    x = min(x, movdpp<DPP_MIRROR>(x));
+    x = min(x, movdpp<DPP_BCAST15, 0xA>(x));
+    x = min(x, movdpp<DPP_BCAST31, 0xC>(x));
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+__device__ __forceinline__ float readlane_f(float x, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
+}
+
+// ------------------------------------------------------------- sweeps
+
+// Position of one path along its scanline.  Horizontal paths are rows;
+// vertical and diagonal paths are indexed by a column g and visit row k at
+// column g (vertical) or (g +/- k) mod W (diagonal): when the column wraps the
+// chain meets the image edge, which is exactly where the reference restarts
+// a diagonal path (SGM.cpp:266,282,330,346), so W chains of H steps cover
+// every pixel once per direction.  `off` is the element offset (i*W + j)*D of
+// the pixel's disparity vector; everything here is wave-uniform (SALU).
+// Correctly rounded x / WIN for the cost filters' window sizes (Solver.cpp:319,
+// 357: sum / win_size).  For WIN = 3 and 5, q0 = x*RN(1/WIN) corrected by one
+// FMA residual step equals IEEE division bit-for-bit for EVERY non-negative
+// finite float (exhaustive GPU check, tools/verify_div.hip; negative x follows
+// by symmetry, and -0 cannot occur in the filters); 3 VALU ops instead of the
+// ~10-op div_scale/div_fmas/div_fixup sequence.
+template <int WIN>
+__device__ __forceinline__ float div_win(float x) {
+    if constexpr (WIN == 1) {
+        return x;
+    } else if constexpr (WIN == 2) {
+        return x * 0.5f;
+    } else {
+        constexpr float r = 1.0f / WIN;
+        const float q0 = x * r;
+        const float e = __builtin_fmaf(-q0, (float)WIN, x);
+        return __builtin_fmaf(e, r, q0);
+    }
+}
+
+// Integer division has no scalar instruction, so hipcc computes % in VALU
+// and then treats the (uniform) result as divergent; pin it back to an SGPR.
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <int DIR>
+struct Cursor {
+    int i, j, k;
+    long long off;
+    __device__ __forceinline__ void init(int path, int H, int W, int D) {
+        k = 0;
+        if (DIR == 0) { i = path; j = 0; }
+        else if (DIR == 1) { i = path; j = W - 1; }
+        else if (DIR == 2 || DIR == 4 || DIR == 5) { i = 0; j = path; }
+        else { i = H - 1; j = path; }
+        off = ((long long)i * W + j) * D;
+    }
+    // Position the cursor at step k of chain `path` (forward directions only:
+    // L1 row walk, L3 column walk, L5 / L6 wrapped diagonals).
+    __device__ __forceinline__ void init_at(int path, int kk, int H, int W, int D) {
+        k = kk;
+        if (DIR == 0) { i = path; j = kk; }
+        else if (DIR == 2) { i = kk; j = path; }
+        else if (DIR == 4) { i = kk; j = uniform((path + kk) % W); }
+        else { i = kk; j = uniform(((path - kk) % W + W) % W); }  // DIR 5
+        off = ((long long)i * W + j) * D;
+    }
+    __device__ __forceinline__ bool start(int W) const {
+        if (k == 0) return true;
+        if (DIR == 4 || DIR == 6) return j == 0;
+        if (DIR == 5 || DIR == 7) return j == W - 1;
+        return false;
+    }
+    __device__ __forceinline__ void advance(int W, long long D, long long WD) {
+        // branch-free (scalar selects): a branch here makes hipcc duplicate
+        // the surrounding loads into both arms and lose exact wait counts
+        ++k;
+        switch (DIR) {
+        case 0: ++j; off += D; break;
+        case 1: --j; off -= D; break;
+        case 2: ++i; off += WD; break;
+        case 3: --i; off -= WD; break;
+        case 4:
+        case 6: {
+            const long long di = DIR == 4 ? WD : -WD;
+            const bool wrap = j == W - 1;
+            off += di + (wrap ? -(long long)(W - 1) * D : D);
+            j = wrap ? 0 : j + 1;
+            i += DIR == 4 ? 1 : -1;
+            break;
+        }
+        default: {
+            const long long di = DIR == 5 ? WD : -WD;
+            const bool wrap = j == 0;
+            off += di + (wrap ? (long long)(W - 1) * D : -D);
+            j = wrap ? W - 1 : j - 1;
+            i += DIR == 5 ? 1 : -1;
+            break;
+        }
+        }
+    }
+    // advance only while k < n-1 (prefetch cursors stop on the last pixel)
+    __device__ __forceinline__ void advance_upto(int n, int W, long long D, long long WD) {
+        advance_if(k < n - 1, W, D, WD);
+    }
+    // predicated advance, select-based (no branch)
+    __device__ __forceinline__ void advance_if(bool go, int W, long long D, long long WD) {
+        Cursor nx = *this;
+        nx.advance(W, D, WD);
+        i = go ? nx.i : i;
+        j = go ? nx.j : j;
+        off = go ? nx.off : off;
+        k = go ? nx.k : k;
+    }
+};
+
+template <int V>
+__device__ __forceinline__ void load_v(float (&dst)[V], const float *p, bool active) {
+    if constexpr (V == 4) {
+        float4 t = active ? *reinterpret_cast<const float4 *>(p) : make_float4(SGM_INF, SGM_INF, SGM_INF, SGM_INF);
+        dst[0] = t.x; dst[1] = t.y; dst[2] = t.z; dst[3] = t.w;
+    } else if constexpr (V == 2) {
+        float2 t = active ? *reinterpret_cast<const float2 *>(p) : make_float2(SGM_INF, SGM_INF);
+        dst[0] = t.x; dst[1] = t.y;
+    } else {
+        dst[0] = active ? *p : SGM_INF;
+    }
+}
+
+// V consecutive floats to LDS (16-byte aligned rows)
+template <int V>
+__device__ __forceinline__ void store_lds_v(float *dst, const float (&t)[V]) {
+    if constexpr (V == 4) *reinterpret_cast<float4 *>(dst) = make_float4(t[0], t[1], t[2], t[3]);
+    else if constexpr (V == 2) *reinterpret_cast<float2 *>(dst) = make_float2(t[0], t[1]);
+    else dst[0] = t[0];
+}
+
+template <int V>
+__device__ __forceinline__ void store_v(float *p, const float (&v)[V], bool active) {
+    if (!active) return;
+    if constexpr (V == 4) *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    else if constexpr (V == 2) *reinterpret_cast<float2 *>(p) = make_float2(v[0], v[1]);
+    else *p = v[0];
+}
+
+// One DP step of SGM.cpp:93-117 for the V disparities a lane holds
+// (d = lane*V + v).  The reference's
+//   MIN(MIN(MIN(Lp[d], Lp[d-1]+P1), Lp[d+1]+P1), minLp+P2) + (C - minLp)
+// is evaluated as min3(Lp[d], min(Lp[d-1],Lp[d+1]) + P1, minLp+P2) + (C - minLp):
+// rounding is monotone so min(a,b)+P1 == min(a+P1,b+P1) bit-for-bit, and a
+// missing neighbour at d = 0 / D-1 (the reference clamps to d itself) is
+// +inf, which gives the same minimum because fl(x + P1) >= x.
+template <int V>
+__device__ __forceinline__ void dp_step(const float (&prev)[V], float pmin, const float (&c)[V],
+                                        float (&L)[V], float p1, float p2) {
+    const float left = dppf<DPP_WAVE_SHR1>(SGM_INF, prev[V - 1]);
+    const float right = dppf<DPP_WAVE_SHL1>(SGM_INF, prev[0]);
+    const float pmin_p2 = pmin + p2;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const float dm = v == 0 ? left : prev[v - 1];
+        const float dp = v == V - 1 ? right : prev[v + 1];
+        const float t = fminf(dm, dp) + p1;
+        const float m = fminf(fminf(prev[v], t), pmin_p2);
+        L[v] = m + (c[v] - pmin);
+    }
+}
+
+template <int V>
+__device__ __forceinline__ float pick(const float (&x)[V], int v) {
+    float r = x[0];
+#pragma unroll
+    for (int k = 1; k < V; ++k) r = v == k ? x[k] : r;
+    return r;
+}
+
+// Aggregated WTA + uniqueness (SGM.cpp:376-418) and compute_subpixel
+// (Solver.cpp:577-593) for one pixel whose total cost vector is spread over
+// the wave (d = lane*V + v); everything after the two wave minima is scalar:
+// the first index holding a value is the lowest set bit of a ballot.
+// Lanes without data hold +inf (never equal to a finite minimum).
+template <int V>
+__device__ __forceinline__ int first_index(const float (&tot)[V], float x) {
+    int best = INT_MAX;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const unsigned long long m = __ballot(tot[v] == x);
+        const int cand = m ? (int)__builtin_ctzll(m) * V + v : INT_MAX;
+        best = cand < best ? cand : best;
+    }
+    return best;
+}
+
+template <int V>
+__device__ __forceinline__ void wta_subpixel(const float (&tot)[V], int D, float uniq,
+                                             int &disp_out, float &sub_out) {
+    float lm = tot[0];
+#pragma unroll
+    for (int v = 1; v < V; ++v) lm = fminf(lm, tot[v]);
+    const float m = wave_min_u(lm);
+    float ls = SGM_INF;
+#pragma unroll
+    for (int v = 0; v < V; ++v) ls = fminf(ls, tot[v] != m ? tot[v] : SGM_INF);
+    const float sec = wave_min_u(ls);
+    const int min_d = first_index<V>(tot, m);
+    int d = min_d;
+    if (sec != SGM_INF) {  // a second distinct value exists (else sec = FLT_MAX: ratio ~ 0)
+        const int sec_d = first_index<V>(tot, sec);
+        if (m / sec > uniq && abs(min_d - sec_d) > 1) d = D + 1;
+    }
+    float f;
+    if (d > D - 1) {
+        f = (float)(D + 1);
+    } else if (d == 0 || d == D - 1) {
+        f = (float)d;
+    } else {
+        const float a = readlane_f(pick(tot, (d - 1) % V), (d - 1) / V);
+        const float b = readlane_f(pick(tot, (d + 1) % V), (d + 1) / V);
+        const float c = readlane_f(pick(tot, d % V), d / V);
+        const float x = d + (a - b) / (2 * (a + b - 2 * c));
+        const float lim = (D - 1) * 1.f;
+        f = (lim < x) ? lim : x;  // std::min(x, lim)
+    }
+    disp_out = d;
+    sub_out = f;
+}
+
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its
+// global loads (the prefetch ring stays in flight across the barrier).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Partial WTA state over a set of disparities: the minimum m and the first
+// index i holding it, and the smallest value s != m with its first index si
+// (SGM.cpp:383-408: min_cost/min_d, sec_min_cost/sec_min_d).
+struct Wta {
+    float m, s;
+    int i, si;
+};
+
+// Combine two disjoint partial states (ties go to the lower index, so the
+// merge is symmetric and any lane pairing may be used).
+__device__ __forceinline__ Wta wta_merge(const Wta &A, const Wta &B) {
+    // branch-free selects (a pointer-select here made hipcc spill to scratch)
+    const bool a_lt = A.m < B.m, b_lt = B.m < A.m;
+    Wta r;
+    r.m = fminf(A.m, B.m);
+    r.i = a_lt ? A.i : (b_lt ? B.i : min(A.i, B.i));
+    const float c1 = b_lt ? B.s : A.s;
+    const int j1 = b_lt ? B.si : A.si;
+    const float c2 = a_lt ? B.m : (b_lt ? A.m : B.s);
+    const int j2 = a_lt ? B.i : (b_lt ? A.i : B.si);
+    r.s = fminf(c1, c2);
+    r.si = c1 < c2 ? j1 : (c2 < c1 ? j2 : min(j1, j2));
+    return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ Wta wta_dpp(const Wta &x) {
+    Wta y;
+    y.m = movdppf<CTRL>(x.m);
+    y.s = movdppf<CTRL>(x.s);
+    y.i = movdpp<CTRL>(x.i);
+    y.si = movdpp<CTRL>(x.si);
+    return wta_merge(x, y);
+}
+
+// LDS image of one chunk: PF pixels x D total costs, rows padded by 16 bytes
+// so the consumer's per-pixel reads spread over all banks.
+template <int V>
+constexpr int tbuf_stride() { return 64 * V + 4; }
+
+// WTA + uniqueness + sub-pixel (SGM.cpp:376-418, Solver.cpp:577-593) for
+// `cnt` <= PF pixels whose total cost vectors sit in LDS rows tb[0..cnt), all
+// at once: 64/PF lanes per pixel, each scanning D*PF/64 costs in ascending d,
+// the partial states merged with DPP.  Pixel positions come from pb.
+template <int V, int PF>
+__device__ __forceinline__ void wta_consume_chunk(const float (*tb)[tbuf_stride<V>()],
+                                                  const long long *pb, int cnt, int lane,
+                                                  int Dn, float uniq, uint16_t *disp,
+                                                  float *sub) {
+    constexpr int LPP = 64 / PF;  // lanes per pixel
+    const int Q = Dn / LPP;       // disparities per lane (>= 8)
+    const int px = lane / LPP, q = lane - px * LPP;
+    const int d0 = q * Q;
+    const float *row = tb[px < cnt ? px : 0];
+    Wta w;
+    w.m = SGM_INF; w.s = SGM_INF; w.i = INT_MAX; w.si = INT_MAX;
+    for (int k = 0; k < Q; k += 4) {
+        const float4 x4 = *reinterpret_cast<const float4 *>(row + d0 + k);
+        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = xs[e];
+            const int d = d0 + k + e;
+            const bool lt = x < w.m;
+            const bool sec = !lt && x != w.m && x < w.s;
+            w.s = lt ? w.m : (sec ? x : w.s);
+            w.si = lt ? w.i : (sec ? d : w.si);
+            w.m = lt ? x : w.m;
+            w.i = lt ? d : w.i;
+        }
+    }
+    w = wta_dpp<DPP_QP_1032>(w);
+    w = wta_dpp<DPP_QP_2301>(w);
+    if (LPP == 8) w = wta_dpp<DPP_HALF_MIRROR>(w);
+    int d = w.i;
+    if (w.s != SGM_INF && w.m / w.s > uniq && abs(w.i - w.si) > 1) d = Dn + 1;
+    float f;
+    if (d > Dn - 1) {
+        f = (float)(Dn + 1);
+    } else if (d == 0 || d == Dn - 1) {
+        f = (float)d;
+    } else {
+        const float av = row[d - 1], bv = row[d + 1], cv = row[d];
+        const float x = d + (av - bv) / (2 * (av + bv - 2 * cv));
+        const float lim = (Dn - 1) * 1.f;
+        f = (lim < x) ? lim : x;  // std::min(x, lim)
+    }
+    if (q == 0 && px < cnt) {
+        const long long pix = pb[px];
+        disp[pix] = (uint16_t)d;
+        sub[pix] = f;
+    }
+}
+
+}  // namespace sgm

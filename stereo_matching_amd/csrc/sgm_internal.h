@@ -19,7 +19,7 @@ enum SweepMode {
     SWEEP_STORE_L = 0,  // write L_r and minL_r (parity tests)
     SWEEP_INIT = 1,     // acc_out = L_r
     SWEEP_ACC = 2,      // acc_out = acc_in + L_r   (acc_in may alias acc_out)
-    SWEEP_FINAL = 3     // total = S + (T + L_r) -> WTA, uniqueness, sub-pixel
+    SWEEP_FINAL = 3     // (retired: the final pass is the PAIR_V backward kernel)
 };
 
 struct SweepArgs {
@@ -33,12 +33,51 @@ struct SweepArgs {
     float p1, p2, uniq;
 };
 
+// Scanline families fused into forward/backward pairs (DESIGN.md "Pairs"):
+// the forward direction stores its path state every K steps (checkpoints),
+// the backward kernel recomputes each K-step segment of the forward costs from
+// its checkpoint in registers and combines both on the fly.
+enum PairFamily {
+    PAIR_H = 0,   // L1 (->) forward, L2 (<-) backward, one chain per row
+    PAIR_V = 1,   // L3 (down) forward, L4 (up) backward, one chain per column
+    PAIR_D2 = 2   // L6 (down-left) forward, L7 (up-right) backward, wrapped anti-diagonals
+};
+enum PairMode {
+    PAIR_INIT2 = 0,  // out = Lf + Lb                         (S12 = L1 + L2)
+    PAIR_ACC = 1,    // out = (acc_in + Lf) + Lb              (T = (T5 + L6) + L7)
+    PAIR_FINAL = 2   // total = ((s_in + Lf) + Lb) + acc_in   (S + T) -> WTA, sub-pixel
+};
+
+struct PairArgs {
+    const float *cost;
+    const float *acc_in;
+    const float *s_in;
+    float *out;
+    float *ckpt;
+    uint16_t *disp;
+    float *sub;
+    float p1, p2, uniq;
+};
+
+// floats of checkpoint storage a family needs
+size_t pair_ckpt_floats(int family, Geom g);
+hipError_t launch_pair_fwd(int family, const PairArgs &a, Geom g, hipStream_t st);
+hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipStream_t st);
+// cost_vertical_filter (Solver.cpp:333-368) fused with the L3 forward pass:
+// in = horizontally filtered volume, out = final cost volume, a.ckpt = L3
+// checkpoints.
+// Multi-role launches of the frame schedule (sgm_pair.hip).
+hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
+                          hipStream_t st);
+hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st);
+hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st);
+
 hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64_t *ct,
                          hipStream_t st);
 hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                          int sky_pitch, int view, int filter, Geom g, float *out,
                          hipStream_t st);
-hipError_t launch_cost_v(const float *in, float *out, int filter, Geom g, hipStream_t st);
+hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st);
 hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream_t st);
 hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
                      Geom g, hipStream_t st);

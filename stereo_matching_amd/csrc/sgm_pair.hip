@@ -1,0 +1,263 @@
+// sgm_pair.hip -- forward/backward path pairs with checkpoint recompute.
+//
+// Two opposite directions on the same scanlines (L1/L2 rows, L3/L4 columns,
+// L6/L7 wrapped anti-diagonals) are computed by one forward kernel that only
+// stores its path state every K steps, and one backward kernel that, per
+// K-step segment, recomputes the forward costs from the checkpoint into
+// registers (reading each cost once for both directions) and combines
+//   S12 = L1 + L2, T = (T5 + L6) + L7, total = ((S12 + L3) + L4) + T
+// on the fly -- the reference's association order (SGM.cpp:386-390) -- so no
+// single-direction volume is ever written (DESIGN.md "Pairs").
+//
+// Segments are counted from the END of a chain of n steps: segment 0 covers
+// positions [0, r0) with r0 = n - (nseg-1)*K, segment s >= 1 covers
+// [r0 + (s-1)K, r0 + sK).  Checkpoint m (0 <= m < nseg-1) is the forward state
+// after position r0-1 + mK and seeds segment m+1.  The backward pass therefore
+// meets full segments first and the partial one last.
+#include "sgm_bodies.h"
+
+namespace sgm {
+
+static inline int vals_per_lane(int D) { return D >= 256 ? 4 : (D >= 128 ? 2 : 1); }
+static inline int chain_len(int family, Geom g) { return family == PAIR_H ? g.W : g.H; }
+static inline int num_chains(int family, Geom g) { return family == PAIR_H ? g.H : g.W; }
+
+size_t pair_ckpt_floats(int family, Geom g) {
+    const int K = vals_per_lane(g.D) >= 4 ? 8 : 16;
+    const int n = chain_len(family, g);
+    const size_t nseg = (size_t)((n + K - 1) / K);
+    return (size_t)num_chains(family, g) * nseg * g.D;
+}
+
+// ------------------------------------------------------------ kernels
+
+// cost_vertical_filter (Solver.cpp:333-368) fused with the L3 forward pass
+// (SGM.cpp:161-199): one wave per column, lane l owning the V vertical IIR
+// chains d = l*V .. l*V+V-1.  Row i of the final cost is produced, stored,
+// and fed straight into the L3 DP; L3 is checkpointed for the PAIR_V
+// backward kernel.  The raw rows the IIR adds (raw[i + WIN/2 + 1]) stream
+// through a register ring PF rows ahead.
+template <int V, bool FULL, int WIN, int PF>
+__global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
+                                                  float *__restrict__ out, PairArgs a, Geom g) {
+    constexpr int K = pair_k<V>();
+    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, LA = HALF + 1;
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x;
+    const int H = g.H;
+    const size_t stride = (size_t)g.W * g.D;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+    const float *col = in + (size_t)j * g.D + e0;
+    float *ocol = out + (size_t)j * g.D + e0;
+    const int nseg = (H + K - 1) / K;
+    const int r0 = H - (nseg - 1) * K;
+    float *ck = a.ckpt + (size_t)j * nseg * g.D + e0;
+    int next_ck = r0 - 1, ck_i = 0;
+    const int T = H - 2 * HALF;
+
+    float raw0[V], rawl[V], sum[V], o1[V];
+    load_v<V>(raw0, col, active);
+    load_v<V>(rawl, col + (size_t)(H - 1) * stride, active);  // the only row below LAG+T (WIN=3)
+#pragma unroll
+    for (int v = 0; v < V; ++v) sum[v] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < WIN; ++k) {
+        float r[V];
+        load_v<V>(r, col + (size_t)k * stride, active);
+#pragma unroll
+        for (int v = 0; v < V; ++v) sum[v] += r[v];
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) o1[v] = 0.0f;
+    float ring[PF][V];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        load_v<V>(ring[u], col + (size_t)min(LA + u, H - 1) * stride, active);
+
+    float prev[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+    float pmin = 0.0f;
+
+    auto row = [&](int i, int u, bool refill) {
+        float c[V];
+        if (i < LAG) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) c[v] = raw0[v];
+        } else if (i >= LAG + T) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) c[v] = rawl[v];
+        } else {
+            const int t = i - LAG;
+#pragma unroll
+            for (int v = 0; v < V; ++v) c[v] = div_win<WIN>(sum[v]);
+            if (t < T - 1) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const float sub = LAG == 0 ? c[v] : (t >= 1 ? o1[v] : raw0[v]);
+                    sum[v] = (sum[v] + ring[u][v]) - sub;
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < V; ++v) o1[v] = c[v];
+        }
+        store_v<V>(ocol + (size_t)i * stride, c, active);
+        // L3 forward step on the freshly filtered row
+        float L[V];
+        dp_step<V>(prev, pmin, c, L, a.p1, a.p2);
+#pragma unroll
+        for (int v = 0; v < V; ++v) L[v] = i == 0 ? c[v] : L[v];
+        const float nmin = wave_min(lane_min(L));
+        if (i == next_ck && ck_i < nseg - 1) {
+            store_v<V>(ck + (size_t)ck_i * g.D, L, active);
+            ++ck_i;
+            next_ck += K;
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = L[v];
+        pmin = nmin;
+        if (refill) load_v<V>(ring[u], col + (size_t)min(i + LA + PF, H - 1) * stride, active);
+    };
+    int i0 = 0;
+    for (; i0 + PF <= H; i0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) row(i0 + u, u, true);
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (i0 + u < H) row(i0 + u, u, false);
+}
+
+template <int FD, int V, bool FULL, int PF>
+__global__ __launch_bounds__(64) void pair_fwd_kernel(PairArgs a, Geom g) {
+    pair_fwd_body<FD, V, FULL, PF>(a, g, blockIdx.x);
+}
+
+template <int FAM, int V, bool FULL, int MODE>
+__global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
+    pair_bwd_body<FAM, V, FULL, MODE>(a, g, blockIdx.x, nullptr, nullptr);
+}
+
+// The final pass of a view: PAIR_V backward (L4, recomputing L3) summed with
+// S12 and T, then WTA.  Wave 0 produces total-cost rows into a double-buffered
+// LDS ring, wave 1 runs the batched WTA on the previous chunk.
+template <int V, bool FULL>
+__global__ __launch_bounds__(128) void pair_final_kernel(PairArgs a, Geom g) {
+    __shared__ __attribute__((aligned(16))) float tbuf[2][K_OF(V)][tbuf_stride<V>()];
+    __shared__ long long pbuf[2][K_OF(V)];
+    pair_bwd_body<PAIR_V, V, FULL, PAIR_FINAL>(a, g, blockIdx.x, tbuf, pbuf);
+}
+
+// Multi-role stage kernels of the frame schedule: block ranges run different
+// (independent) roles, so a latency-bound horizontal role (H chains, few and
+// long) overlaps the bandwidth-bound diagonal roles inside one launch.  The
+// H blocks come first so they start at once.
+//   stage A: L1 forward (ckpt)  |  L5 -> T5         |  L6 forward (ckpt)
+//   stage B: L2 backward -> S12 |  L7 backward: T = (T5 + L6) + L7
+template <int V, bool FULL>
+__global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, PairArgs d6,
+                                                     Geom g) {
+    constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
+    int b = blockIdx.x;
+    if (b < g.H) {
+        pair_fwd_body<0, V, FULL, PFH>(h1, g, b);
+        return;
+    }
+    b -= g.H;
+    if (b < g.W) {
+        sweep_body<4, V, SWEEP_INIT, FULL, PFD>(l5, g, b);
+        return;
+    }
+    pair_fwd_body<5, V, FULL, PFD>(d6, g, b - g.W);
+}
+
+template <int V, bool FULL>
+__global__ __launch_bounds__(64) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
+    const int b = blockIdx.x;
+    if (b < g.H) pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, b, nullptr, nullptr);
+    else pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(d7, g, b - g.H, nullptr, nullptr);
+}
+
+hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
+                          hipStream_t st) {
+    const dim3 grid(g.H + 2 * g.W);
+    if (g.D == 32) stage_a_kernel<1, false><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    else if (g.D == 64) stage_a_kernel<1, true><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    else if (g.D == 128) stage_a_kernel<2, true><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    else stage_a_kernel<4, true><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st) {
+    const dim3 grid(g.H + g.W);
+    if (g.D == 32) stage_b_kernel<1, false><<<grid, 64, 0, st>>>(h2, d7, g);
+    else if (g.D == 64) stage_b_kernel<1, true><<<grid, 64, 0, st>>>(h2, d7, g);
+    else if (g.D == 128) stage_b_kernel<2, true><<<grid, 64, 0, st>>>(h2, d7, g);
+    else stage_b_kernel<4, true><<<grid, 64, 0, st>>>(h2, d7, g);
+    return hipGetLastError();
+}
+
+// -------------------------------------------------------------- launch
+
+template <int FD>
+static void launch_fwd_t(const PairArgs &a, Geom g, hipStream_t st) {
+    const dim3 grid(FD == 0 ? g.H : g.W);
+    constexpr int PF = FD == 0 ? 32 : 16;
+    if (g.D == 32) pair_fwd_kernel<FD, 1, false, PF><<<grid, 64, 0, st>>>(a, g);
+    else if (g.D == 64) pair_fwd_kernel<FD, 1, true, PF><<<grid, 64, 0, st>>>(a, g);
+    else if (g.D == 128) pair_fwd_kernel<FD, 2, true, PF><<<grid, 64, 0, st>>>(a, g);
+    else pair_fwd_kernel<FD, 4, true, PF / 2><<<grid, 64, 0, st>>>(a, g);
+}
+
+hipError_t launch_pair_fwd(int family, const PairArgs &a, Geom g, hipStream_t st) {
+    // (the production schedule runs PAIR_V's forward pass fused into the
+    // vertical cost filter, launch_vfwd; this one starts from a final volume)
+    if (family == PAIR_H) launch_fwd_t<0>(a, g, st);
+    else if (family == PAIR_V) launch_fwd_t<2>(a, g, st);
+    else launch_fwd_t<5>(a, g, st);
+    return hipGetLastError();
+}
+
+template <int WIN>
+static void launch_vfwd_t(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st) {
+    const dim3 grid(g.W);
+    if (g.D == 32) vfwd_kernel<1, false, WIN, 16><<<grid, 64, 0, st>>>(in, out, a, g);
+    else if (g.D == 64) vfwd_kernel<1, true, WIN, 16><<<grid, 64, 0, st>>>(in, out, a, g);
+    else if (g.D == 128) vfwd_kernel<2, true, WIN, 16><<<grid, 64, 0, st>>>(in, out, a, g);
+    else vfwd_kernel<4, true, WIN, 8><<<grid, 64, 0, st>>>(in, out, a, g);
+}
+
+hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st) {
+    if (g.scale == 1) launch_vfwd_t<3>(in, out, a, g, st);
+    else launch_vfwd_t<1>(in, out, a, g, st);
+    return hipGetLastError();
+}
+
+template <int FAM, int MODE>
+static void launch_bwd_t(const PairArgs &a, Geom g, hipStream_t st) {
+    const dim3 grid(FAM == PAIR_H ? g.H : g.W);
+    if (g.D == 32) pair_bwd_kernel<FAM, 1, false, MODE><<<grid, 64, 0, st>>>(a, g);
+    else if (g.D == 64) pair_bwd_kernel<FAM, 1, true, MODE><<<grid, 64, 0, st>>>(a, g);
+    else if (g.D == 128) pair_bwd_kernel<FAM, 2, true, MODE><<<grid, 64, 0, st>>>(a, g);
+    else pair_bwd_kernel<FAM, 4, true, MODE><<<grid, 64, 0, st>>>(a, g);
+}
+
+static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
+    const dim3 grid(g.W);
+    if (g.D == 32) pair_final_kernel<1, false><<<grid, 128, 0, st>>>(a, g);
+    else if (g.D == 64) pair_final_kernel<1, true><<<grid, 128, 0, st>>>(a, g);
+    else if (g.D == 128) pair_final_kernel<2, true><<<grid, 128, 0, st>>>(a, g);
+    else pair_final_kernel<4, true><<<grid, 128, 0, st>>>(a, g);
+}
+
+hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipStream_t st) {
+    // the production schedule uses H/INIT2, D2/ACC and V/FINAL
+    if (family == PAIR_H && mode == PAIR_INIT2) launch_bwd_t<PAIR_H, PAIR_INIT2>(a, g, st);
+    else if (family == PAIR_D2 && mode == PAIR_ACC) launch_bwd_t<PAIR_D2, PAIR_ACC>(a, g, st);
+    else if (family == PAIR_V && mode == PAIR_FINAL) launch_final_t(a, g, st);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace sgm

@@ -1,0 +1,96 @@
+// sgm_sweep.hip -- single-direction path sweeps, the fused final sweep, LR check.
+// CDNA4 (gfx950) kernels of the semi-global matcher.
+//
+// Stage map (reference -> kernel), full design in DESIGN.md:
+//   cv::GaussianBlur + CT_pts     Solver.cpp:120-140, cost.cpp:99-129  -> census_kernel
+//   build_dsi_from_table[_beta]   Solver.cpp:143-248
+//     + cost_horizontal_filter    Solver.cpp:296-330                   -> cost_h_kernel
+//   cost_vertical_filter          Solver.cpp:333-368                   -> cost_v_kernel
+//   L1..L8 path DP                SGM.cpp:81-369                       -> sweep_kernel<DIR,..>
+//                                                     (pairs: sgm_pair.hip)
+//   aggregation + WTA + unique    SGM.cpp:372-418
+//     + compute_subpixel          Solver.cpp:569-597                   -> pair_final_kernel
+//   LR check                      SGM.cpp:803-818                      -> lr_kernel
+//
+// Bit-exactness rules (DESIGN.md "Numerics"): built with -ffp-contract=off,
+// no fast-math, correctly rounded f32 division; every float expression keeps
+// the reference's association order.
+#include "sgm_bodies.h"
+
+namespace sgm {
+
+template <int DIR, int V, int MODE, bool FULL, int PF>
+__global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
+    sweep_body<DIR, V, MODE, FULL, PF>(a, g, blockIdx.x);
+}
+
+// Steps of loads kept in flight: horizontal paths (few, long, latency-bound)
+// need a deeper ring than the W column/diagonal paths.
+template <int DIR>
+constexpr int sweep_pf() { return DIR < 2 ? 32 : 16; }
+
+template <int DIR, int MODE>
+static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
+    const dim3 grid(DIR < 2 ? g.H : g.W);
+    constexpr int PF = sweep_pf<DIR>();
+    if (g.D == 32)
+        sweep_kernel<DIR, 1, MODE, false, PF><<<grid, 64, 0, st>>>(a, g);
+    else if (g.D == 64)
+        sweep_kernel<DIR, 1, MODE, true, PF><<<grid, 64, 0, st>>>(a, g);
+    else if (g.D == 128)
+        sweep_kernel<DIR, 2, MODE, true, PF><<<grid, 64, 0, st>>>(a, g);
+    else
+        sweep_kernel<DIR, 4, MODE, true, PF / 2><<<grid, 64, 0, st>>>(a, g);
+}
+
+template <int MODE>
+static void launch_sweep_m(int dir, const SweepArgs &a, Geom g, hipStream_t st) {
+    switch (dir) {
+    case 0: launch_sweep_v<0, MODE>(a, g, st); break;
+    case 1: launch_sweep_v<1, MODE>(a, g, st); break;
+    case 2: launch_sweep_v<2, MODE>(a, g, st); break;
+    case 3: launch_sweep_v<3, MODE>(a, g, st); break;
+    case 4: launch_sweep_v<4, MODE>(a, g, st); break;
+    case 5: launch_sweep_v<5, MODE>(a, g, st); break;
+    case 6: launch_sweep_v<6, MODE>(a, g, st); break;
+    default: launch_sweep_v<7, MODE>(a, g, st); break;
+    }
+}
+
+hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream_t st) {
+    switch (mode) {
+    case SWEEP_STORE_L: launch_sweep_m<SWEEP_STORE_L>(dir, a, g, st); break;
+    case SWEEP_INIT: launch_sweep_m<SWEEP_INIT>(dir, a, g, st); break;
+    case SWEEP_ACC: launch_sweep_m<SWEEP_ACC>(dir, a, g, st); break;
+    default: return hipErrorInvalidValue;  // the final pass is pair_final_kernel
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------- LR check
+
+// SGM.cpp:803-818: dr = FR[i][(int)(j - dl/s)] when j >= dl; invalid if
+// |dl - dr| > LR_CHECK_DIS.
+__global__ __launch_bounds__(256) void lr_kernel(const float *__restrict__ fl,
+                                                 const float *__restrict__ fr,
+                                                 float *__restrict__ out, int out_pitch, int H,
+                                                 int W, int D, int scale, float lr) {
+    const int j = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y;
+    if (j >= W) return;
+    float dl = fl[(size_t)i * W + j];
+    if (j >= dl) {
+        const int jr = clampi((int)(j - dl / scale), 0, W - 1);
+        const float dr = fr[(size_t)i * W + jr];
+        if (fabsf(dl - dr) > lr) dl = (float)(D + 1);
+    }
+    out[(size_t)i * out_pitch + j] = dl;
+}
+
+hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
+                     Geom g, hipStream_t st) {
+    lr_kernel<<<dim3((g.W + 255) / 256, g.H), 256, 0, st>>>(fl, fr, out, out_pitch, g.H, g.W, g.D,
+                                                           g.scale, lr);
+    return hipGetLastError();
+}
+
+}  // namespace sgm
