@@ -48,16 +48,17 @@ CONFIGS = {
 
 # Algorithmic HBM bytes per pixel-disparity element per launch (DESIGN.md
 # "Roofline"): f32 volumes, each read or written once; checkpoints are one
-# D-vector per K steps (K = 16, or 8 at D = 256).
+# D-vector per K steps (H/D2: K = 16, 8 at D = 256; V: K = 8, 4 at D = 256).
 def bytes_per_elem(name: str, D: int) -> float:
-    ck = 4.0 / (8 if D >= 256 else 16)
+    ck = 4.0 / (8 if D >= 256 else 16)      # H and D2 families
+    ckv = 4.0 / (4 if D >= 256 else 8)      # vertical family
     table = {
         "cost_h": 4.0,                  # write C_h (census rows come from LDS)
-        "vfwd": 8.0 + ck,               # read C_h, write C, write L3 checkpoints
-        "pair_fwd_L1": 4.0 + ck, "pair_fwd_L3": 4.0 + ck, "pair_fwd_L6": 4.0 + ck,
+        "vfwd": 8.0 + ckv,              # read C_h, write C, write L3 checkpoints
+        "pair_fwd_L1": 4.0 + ck, "pair_fwd_L3": 4.0 + ckv, "pair_fwd_L6": 4.0 + ck,
         "pair_bwd_L2_init2": 8.0 + ck,  # read C + ckpt, write S12
         "pair_bwd_L7_acc": 12.0 + ck,   # read C + T5 + ckpt, write T
-        "pair_bwd_L4_final": 12.0 + ck,  # read C + S12 + T + ckpt
+        "pair_bwd_L4_final": 12.0 + ckv,  # read C + S12 + T + ckpt
         # multi-role launches (sums of their roles)
         "stage_a": (4.0 + ck) + 8.0 + (4.0 + ck),   # L1 fwd | L5 -> T5 | L6 fwd
         "stage_b": (8.0 + ck) + (12.0 + ck),        # L2 bwd -> S12 | L7 bwd -> T

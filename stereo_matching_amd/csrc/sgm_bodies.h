@@ -10,9 +10,15 @@
 
 namespace sgm {
 
+// Segment length K (steps between checkpoints).  The vertical family's final
+// kernel holds five K x V register arrays, so it uses a shorter K to stay at
+// <= 128 VGPRs (four waves per SIMD).
 template <int V>
 constexpr int pair_k() { return V >= 4 ? 8 : 16; }
-#define K_OF(V) pair_k<V>()
+template <int V>
+constexpr int pair_kv() { return V >= 4 ? 4 : 8; }
+template <int FAM, int V>
+constexpr int family_k() { return FAM == PAIR_V ? pair_kv<V>() : pair_k<V>(); }
 
 template <int V>
 __device__ __forceinline__ float lane_min(const float (&x)[V]) {
@@ -130,7 +136,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 // output is the checkpoint set.
 template <int FD, int V, bool FULL, int PF>
 __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, int path) {
-    constexpr int K = pair_k<V>();
+    constexpr int K = family_k<FD == 0 ? PAIR_H : (FD == 2 ? PAIR_V : PAIR_D2), V>();
     const int lane = threadIdx.x & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -193,11 +199,11 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
 // pixel positions), unused otherwise.
 template <int FAM, int V, bool FULL, int MODE>
 __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, int path,
-                                              float (*tb)[K_OF(V)][tbuf_stride<V>()],
-                                              long long (*pb)[K_OF(V)]) {
+                                              float (*tb)[family_k<FAM, V>()][tbuf_stride<V>()],
+                                              long long (*pb)[family_k<FAM, V>()]) {
     constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
     constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
-    constexpr int K = pair_k<V>();
+    constexpr int K = family_k<FAM, V>();
     constexpr bool FINAL = MODE == PAIR_FINAL;
     constexpr bool NEED_ACC = MODE != PAIR_INIT2;
     constexpr bool NEED_S = FINAL;
@@ -356,6 +362,200 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
         process_seg(c0, 0, part_t{});
     }
     if (FINAL) lds_barrier();
+}
+
+// ------------------------------------------------- split pair backward
+//
+// The same backward pass with its two serial chains on two waves of one
+// workgroup: wave 0 (producer) recomputes each forward segment from its
+// checkpoint and writes the segment's costs and forward path costs to a
+// double-buffered LDS ring; wave 1 (consumer) runs the backward direction over
+// the previous segment and combines (INIT2 / ACC: stores the volume; FINAL:
+// writes total-cost rows to a second LDS ring that wave 2 turns into WTA
+// results).  One serial chain per wave: the pair costs one chain latency.
+//
+// Barrier schedule (every wave runs nseg + NW - 1 LDS barriers): in
+// iteration t the producer fills chunk t, the consumer drains chunk t-1 and
+// the WTA wave chunk t-2 (chunk c = segment nseg-1-c).
+template <int K, int V>
+struct SplitLds {
+    float c[2][K][tbuf_stride<V>()];    // segment costs
+    float l[2][K][tbuf_stride<V>()];    // recomputed forward path costs
+};
+
+template <int K, int V>
+struct SplitFinalLds {
+    SplitLds<K, V> s;
+    float t[2][K][tbuf_stride<V>()];    // total costs for the WTA wave
+    long long p[2][K];                  // their pixel positions
+};
+
+template <int FAM, int V, bool FULL, int MODE, int K>
+__device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g, int path,
+                                                int wave, SplitLds<K, V> &L,
+                                                SplitFinalLds<K, V> *F) {
+    constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
+    constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
+    constexpr bool FINAL = MODE == PAIR_FINAL;
+    constexpr int NW = FINAL ? 3 : 2;
+    constexpr bool NEED_ACC = MODE != PAIR_INIT2;
+    constexpr bool NEED_S = FINAL;
+    const int lane = threadIdx.x & 63;
+    const int H = g.H, W = g.W;
+    const long long D = g.D, WD = (long long)g.W * g.D;
+    const int n = FAM == PAIR_H ? W : H;
+    const int nseg = (n + K - 1) / K;
+    const int r0 = n - (nseg - 1) * K;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+    using full_t = std::integral_constant<bool, true>;
+    using part_t = std::integral_constant<bool, false>;
+
+    if (wave == 0) {
+        // ---------------------------------------------------- producer
+        const float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
+        float c0[K][V], c1[K][V];
+        auto load_seg = [&](float (&cs)[K][V], int s) {
+            const int cnt = s == 0 ? r0 : K;
+            const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
+            Cursor<FD> fc;
+            fc.init_at(path, pos0, H, W, g.D);
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) {
+                load_v<V>(cs[kk], a.cost + fc.off + e0, active);
+                fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
+            }
+        };
+        auto produce = [&](float (&cs)[K][V], int s, auto full_tag) {
+            constexpr bool FULLSEG = decltype(full_tag)::value;
+            const int cnt = FULLSEG ? K : (s == 0 ? r0 : K);
+            const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
+            const int skip = K - cnt;
+            const int buf = (nseg - 1 - s) & 1;
+            float pf[V];
+            float pminf = 0.0f;
+            if (s > 0) {
+                load_v<V>(pf, ck + (size_t)(s - 1) * g.D, active);
+                pminf = wave_min(lane_min(pf));
+            } else {
+#pragma unroll
+                for (int v = 0; v < V; ++v) pf[v] = SGM_INF;
+            }
+            Cursor<FD> fc;
+            fc.init_at(path, pos0, H, W, g.D);
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) {
+                if (FULLSEG || kk >= skip) {
+                    float Lr[V];
+                    dp_step<V>(pf, pminf, cs[kk], Lr, a.p1, a.p2);
+                    const bool st = fc.start(W);
+#pragma unroll
+                    for (int v = 0; v < V; ++v) Lr[v] = st ? cs[kk][v] : Lr[v];
+                    pminf = wave_min(lane_min(Lr));
+                    store_lds_v<V>(&L.c[buf][kk][e0], cs[kk]);
+                    store_lds_v<V>(&L.l[buf][kk][e0], Lr);
+#pragma unroll
+                    for (int v = 0; v < V; ++v) pf[v] = Lr[v];
+                    fc.advance(W, D, WD);
+                }
+            }
+            lds_barrier();
+        };
+        load_seg(c0, nseg - 1);
+        int s = nseg - 1;
+        for (; s >= 2; s -= 2) {
+            load_seg(c1, s - 1);
+            produce(c0, s, full_t{});
+            load_seg(c0, s - 2);
+            produce(c1, s - 1, full_t{});
+        }
+        if (s == 1) {
+            load_seg(c1, 0);
+            produce(c0, 1, full_t{});
+            produce(c1, 0, part_t{});
+        } else {
+            produce(c0, 0, part_t{});
+        }
+#pragma unroll
+        for (int t = 0; t < NW - 1; ++t) lds_barrier();
+    } else if (wave == 1) {
+        // ---------------------------------------------------- consumer
+        const int bpath = FAM == PAIR_D2 ? uniform(((path - (H - 1)) % W + W) % W) : path;
+        Cursor<BD> bc, pc;
+        bc.init(bpath, H, W, g.D);
+        pc.init(bpath, H, W, g.D);
+        float ab[K][V], sb[K][V];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+            if (NEED_S) load_v<V>(sb[u], a.s_in + pc.off + e0, active);
+            pc.advance_upto(n, W, D, WD);
+        }
+        float prevb[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
+        float pminb = 0.0f;
+        auto consume = [&](int c, auto full_tag) {
+            constexpr bool FULLSEG = decltype(full_tag)::value;
+            const int cnt = FULLSEG ? K : (c == nseg - 1 ? r0 : K);
+            const int skip = K - cnt;
+            const int buf = c & 1;
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const int kk = K - 1 - r;
+                if (FULLSEG || kk >= skip) {
+                    float cs[V], lf[V];
+                    load_lds_v<V>(cs, &L.c[buf][kk][e0]);
+                    load_lds_v<V>(lf, &L.l[buf][kk][e0]);
+                    float Lr[V];
+                    dp_step<V>(prevb, pminb, cs, Lr, a.p1, a.p2);
+                    const bool st = bc.start(W);
+#pragma unroll
+                    for (int v = 0; v < V; ++v) Lr[v] = st ? cs[v] : Lr[v];
+                    const float nmin = wave_min(lane_min(Lr));
+                    if constexpr (MODE == PAIR_INIT2) {
+                        float o[V];
+#pragma unroll
+                        for (int v = 0; v < V; ++v) o[v] = lf[v] + Lr[v];
+                        store_v<V>(a.out + bc.off + e0, o, active);
+                    } else if constexpr (MODE == PAIR_ACC) {
+                        float o[V];
+#pragma unroll
+                        for (int v = 0; v < V; ++v) o[v] = (ab[r][v] + lf[v]) + Lr[v];
+                        store_v<V>(a.out + bc.off + e0, o, active);
+                    } else {
+                        float tot[V];
+#pragma unroll
+                        for (int v = 0; v < V; ++v) tot[v] = ((sb[r][v] + lf[v]) + Lr[v]) + ab[r][v];
+                        store_lds_v<V>(&F->t[buf][r][e0], tot);
+                        if (lane == 0) F->p[buf][r] = (long long)bc.i * W + bc.j;
+                    }
+#pragma unroll
+                    for (int v = 0; v < V; ++v) prevb[v] = Lr[v];
+                    pminb = nmin;
+                    bc.advance(W, D, WD);
+                    if (NEED_ACC) load_v<V>(ab[r], a.acc_in + pc.off + e0, active);
+                    if (NEED_S) load_v<V>(sb[r], a.s_in + pc.off + e0, active);
+                    pc.advance_upto(n, W, D, WD);
+                }
+            }
+            lds_barrier();
+        };
+        lds_barrier();
+        int c = 0;
+        for (; c < nseg - 1; ++c) consume(c, full_t{});
+        consume(nseg - 1, part_t{});
+        if (FINAL) lds_barrier();
+    } else if constexpr (FINAL) {
+        // ------------------------------------------------- WTA (wave 2)
+        lds_barrier();
+        lds_barrier();
+        for (int c = 0; c < nseg; ++c) {
+            wta_consume_chunk<V, K>(F->t[c & 1], F->p[c & 1], c == nseg - 1 ? r0 : K, lane, g.D,
+                                    a.uniq, a.disp, a.sub);
+            lds_barrier();
+        }
+    }
 }
 
 }  // namespace sgm

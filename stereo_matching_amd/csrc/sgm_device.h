@@ -203,6 +203,20 @@ __device__ __forceinline__ void load_v(float (&dst)[V], const float *p, bool act
     }
 }
 
+// V consecutive floats from LDS
+template <int V>
+__device__ __forceinline__ void load_lds_v(float (&t)[V], const float *src) {
+    if constexpr (V == 4) {
+        const float4 x = *reinterpret_cast<const float4 *>(src);
+        t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w;
+    } else if constexpr (V == 2) {
+        const float2 x = *reinterpret_cast<const float2 *>(src);
+        t[0] = x.x; t[1] = x.y;
+    } else {
+        t[0] = src[0];
+    }
+}
+
 // V consecutive floats to LDS (16-byte aligned rows)
 template <int V>
 __device__ __forceinline__ void store_lds_v(float *dst, const float (&t)[V]) {
@@ -383,7 +397,8 @@ __device__ __forceinline__ void wta_consume_chunk(const float (*tb)[tbuf_stride<
     }
     w = wta_dpp<DPP_QP_1032>(w);
     w = wta_dpp<DPP_QP_2301>(w);
-    if (LPP == 8) w = wta_dpp<DPP_HALF_MIRROR>(w);
+    if (LPP >= 8) w = wta_dpp<DPP_HALF_MIRROR>(w);
+    if (LPP >= 16) w = wta_dpp<DPP_MIRROR>(w);
     int d = w.i;
     if (w.s != SGM_INF && w.m / w.s > uniq && abs(w.i - w.si) > 1) d = Dn + 1;
     float f;

@@ -23,7 +23,8 @@ static inline int chain_len(int family, Geom g) { return family == PAIR_H ? g.W 
 static inline int num_chains(int family, Geom g) { return family == PAIR_H ? g.H : g.W; }
 
 size_t pair_ckpt_floats(int family, Geom g) {
-    const int K = vals_per_lane(g.D) >= 4 ? 8 : 16;
+    const int V = vals_per_lane(g.D);
+    const int K = family == PAIR_V ? (V >= 4 ? 4 : 8) : (V >= 4 ? 8 : 16);
     const int n = chain_len(family, g);
     const size_t nseg = (size_t)((n + K - 1) / K);
     return (size_t)num_chains(family, g) * nseg * g.D;
@@ -40,7 +41,7 @@ size_t pair_ckpt_floats(int family, Geom g) {
 template <int V, bool FULL, int WIN, int PF>
 __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
                                                   float *__restrict__ out, PairArgs a, Geom g) {
-    constexpr int K = pair_k<V>();
+    constexpr int K = pair_kv<V>();
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, LA = HALF + 1;
     const int lane = threadIdx.x;
     const int j = blockIdx.x;
@@ -144,8 +145,8 @@ __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
 // LDS ring, wave 1 runs the batched WTA on the previous chunk.
 template <int V, bool FULL>
 __global__ __launch_bounds__(128) void pair_final_kernel(PairArgs a, Geom g) {
-    __shared__ __attribute__((aligned(16))) float tbuf[2][K_OF(V)][tbuf_stride<V>()];
-    __shared__ long long pbuf[2][K_OF(V)];
+    __shared__ __attribute__((aligned(16))) float tbuf[2][pair_kv<V>()][tbuf_stride<V>()];
+    __shared__ long long pbuf[2][pair_kv<V>()];
     pair_bwd_body<PAIR_V, V, FULL, PAIR_FINAL>(a, g, blockIdx.x, tbuf, pbuf);
 }
 
