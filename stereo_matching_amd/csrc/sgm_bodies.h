@@ -245,7 +245,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
         pc.advance_upto(n, W, D, WD);
     }
 
-    float c0[K][V], c1[K][V], lf[K][V];
+    float c0[K + 1][V], c1[K + 1][V], lf[K][V];
     float prevb[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
@@ -254,7 +254,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     // costs of segment s into cs; array slot kk holds position
     // pos0 + kk - (K - cnt) (slots below K - cnt are unused for the partial
     // segment and load position pos0 again)
-    auto load_seg = [&](float (&cs)[K][V], int s) {
+    auto load_seg = [&](float (&cs)[K + 1][V], int s) {
         const int cnt = s == 0 ? r0 : K;
         const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
         Cursor<FD> fc;
@@ -264,9 +264,12 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
             load_v<V>(cs[kk], a.cost + fc.off + e0, active);
             fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
         }
+        // slot K: the checkpoint seeding the segment, fetched with its costs
+        // so recomputation never waits on a load younger than the look-ahead
+        load_v<V>(cs[K], ck + (size_t)(s > 0 ? s - 1 : 0) * g.D, active);
     };
 
-    auto process_seg = [&](float (&cs)[K][V], int s, auto full_tag) {
+    auto process_seg = [&](float (&cs)[K + 1][V], int s, auto full_tag) {
         constexpr bool FULLSEG = decltype(full_tag)::value;
         const int cnt = FULLSEG ? K : (s == 0 ? r0 : K);
         const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
@@ -274,10 +277,11 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
         // 1) recompute the forward costs of this segment from its checkpoint
         float pf[V];
         float pminf = 0.0f;
-        if (s > 0) {
-            load_v<V>(pf, ck + (size_t)(s - 1) * g.D, active);
+        if constexpr (FULLSEG) {  // s >= 1
+#pragma unroll
+            for (int v = 0; v < V; ++v) pf[v] = cs[K][v];
             pminf = wave_min(lane_min(pf));
-        } else {
+        } else {  // segment 0 starts the chain
 #pragma unroll
             for (int v = 0; v < V; ++v) pf[v] = SGM_INF;
         }
@@ -390,10 +394,15 @@ struct SplitFinalLds {
     long long p[2][K];                  // their pixel positions
 };
 
-template <int FAM, int V, bool FULL, int MODE, int K>
+// NB: register buffers of segment costs in the producer (NB-1 segments of
+// loads in flight while one is recomputed); RH: the consumer's ring of
+// accumulator loads is RH*K steps deep (chunks processed RH at a time).
+template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1>
 __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g, int path,
                                                 int wave, SplitLds<K, V> &L,
                                                 SplitFinalLds<K, V> *F) {
+    static_assert(NB == 2 || NB == 3, "producer buffers");
+    static_assert(RH == 1 || RH == 2, "consumer ring halves");
     constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
     constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
     constexpr bool FINAL = MODE == PAIR_FINAL;
@@ -414,8 +423,14 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     if (wave == 0) {
         // ---------------------------------------------------- producer
         const float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
-        float c0[K][V], c1[K][V];
-        auto load_seg = [&](float (&cs)[K][V], int s) {
+        float cb[NB][K + 1][V];
+        // segment s (clamped at 0: look-ahead past the last segment reloads
+        // segment 0 into a buffer nobody reads, keeping the loop branch-free);
+        // slot K holds the checkpoint seeding the segment, fetched with its
+        // costs so recomputation never waits on a load younger than the
+        // look-ahead
+        auto load_seg = [&](float (&cs)[K + 1][V], int s) {
+            s = s < 0 ? 0 : s;
             const int cnt = s == 0 ? r0 : K;
             const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
             Cursor<FD> fc;
@@ -425,8 +440,9 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                 load_v<V>(cs[kk], a.cost + fc.off + e0, active);
                 fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
             }
+            load_v<V>(cs[K], ck + (size_t)(s > 0 ? s - 1 : 0) * g.D, active);
         };
-        auto produce = [&](float (&cs)[K][V], int s, auto full_tag) {
+        auto produce = [&](float (&cs)[K + 1][V], int s, auto full_tag) {
             constexpr bool FULLSEG = decltype(full_tag)::value;
             const int cnt = FULLSEG ? K : (s == 0 ? r0 : K);
             const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
@@ -434,10 +450,11 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             const int buf = (nseg - 1 - s) & 1;
             float pf[V];
             float pminf = 0.0f;
-            if (s > 0) {
-                load_v<V>(pf, ck + (size_t)(s - 1) * g.D, active);
+            if constexpr (FULLSEG) {  // s >= 1
+#pragma unroll
+                for (int v = 0; v < V; ++v) pf[v] = cs[K][v];
                 pminf = wave_min(lane_min(pf));
-            } else {
+            } else {  // segment 0 starts the chain
 #pragma unroll
                 for (int v = 0; v < V; ++v) pf[v] = SGM_INF;
             }
@@ -461,32 +478,49 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             }
             lds_barrier();
         };
-        load_seg(c0, nseg - 1);
+        // buffer u holds segment nseg-1-m for m = u (mod NB)
+#pragma unroll
+        for (int u = 0; u + 1 < NB; ++u) load_seg(cb[u], nseg - 1 - u);
         int s = nseg - 1;
-        for (; s >= 2; s -= 2) {
-            load_seg(c1, s - 1);
-            produce(c0, s, full_t{});
-            load_seg(c0, s - 2);
-            produce(c1, s - 1, full_t{});
+        // full segments NB at a time, each step first issuing the segment
+        // NB-1 further down
+        for (; s - (NB - 1) >= 1; s -= NB) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                load_seg(cb[(u + NB - 1) % NB], s - u - (NB - 1));
+                produce(cb[u], s - u, full_t{});
+            }
         }
-        if (s == 1) {
-            load_seg(c1, 0);
-            produce(c0, 1, full_t{});
-            produce(c1, 0, part_t{});
-        } else {
-            produce(c0, 0, part_t{});
-        }
+        // fewer than NB segments left (s + 1 of them, the last partial)
+        auto tail = [&](auto u_tag) {
+            constexpr int U = decltype(u_tag)::value;
+            if constexpr (U < NB) {
+                if (s >= 1) {
+                    load_seg(cb[(U + NB - 1) % NB], s - (NB - 1));
+                    produce(cb[U], s, full_t{});
+                    --s;
+                }
+            }
+        };
+        tail(std::integral_constant<int, 0>{});
+        if constexpr (NB == 3) tail(std::integral_constant<int, 1>{});
+        // segment 0 is in buffer (nseg - 1) % NB
+        const int b0 = (nseg - 1) % NB;
+        if (b0 == 0) produce(cb[0], 0, part_t{});
+        else if (b0 == 1) produce(cb[1], 0, part_t{});
+        else produce(cb[NB - 1], 0, part_t{});
 #pragma unroll
         for (int t = 0; t < NW - 1; ++t) lds_barrier();
     } else if (wave == 1) {
         // ---------------------------------------------------- consumer
+        constexpr int RD = RH * K;
         const int bpath = FAM == PAIR_D2 ? uniform(((path - (H - 1)) % W + W) % W) : path;
         Cursor<BD> bc, pc;
         bc.init(bpath, H, W, g.D);
         pc.init(bpath, H, W, g.D);
-        float ab[K][V], sb[K][V];
+        float ab[RD][V], sb[RD][V];
 #pragma unroll
-        for (int u = 0; u < K; ++u) {
+        for (int u = 0; u < RD; ++u) {
             if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
             if (NEED_S) load_v<V>(sb[u], a.s_in + pc.off + e0, active);
             pc.advance_upto(n, W, D, WD);
@@ -495,8 +529,9 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
 #pragma unroll
         for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
         float pminb = 0.0f;
-        auto consume = [&](int c, auto full_tag) {
+        auto consume = [&](int c, auto full_tag, auto half_tag) {
             constexpr bool FULLSEG = decltype(full_tag)::value;
+            constexpr int HF = decltype(half_tag)::value;
             const int cnt = FULLSEG ? K : (c == nseg - 1 ? r0 : K);
             const int skip = K - cnt;
             const int buf = c & 1;
@@ -504,6 +539,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             for (int r = 0; r < K; ++r) {
                 const int kk = K - 1 - r;
                 if (FULLSEG || kk >= skip) {
+                    const int q = HF * K + r;   // ring slot
                     float cs[V], lf[V];
                     load_lds_v<V>(cs, &L.c[buf][kk][e0]);
                     load_lds_v<V>(lf, &L.l[buf][kk][e0]);
@@ -521,12 +557,12 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     } else if constexpr (MODE == PAIR_ACC) {
                         float o[V];
 #pragma unroll
-                        for (int v = 0; v < V; ++v) o[v] = (ab[r][v] + lf[v]) + Lr[v];
+                        for (int v = 0; v < V; ++v) o[v] = (ab[q][v] + lf[v]) + Lr[v];
                         store_v<V>(a.out + bc.off + e0, o, active);
                     } else {
                         float tot[V];
 #pragma unroll
-                        for (int v = 0; v < V; ++v) tot[v] = ((sb[r][v] + lf[v]) + Lr[v]) + ab[r][v];
+                        for (int v = 0; v < V; ++v) tot[v] = ((sb[q][v] + lf[v]) + Lr[v]) + ab[q][v];
                         store_lds_v<V>(&F->t[buf][r][e0], tot);
                         if (lane == 0) F->p[buf][r] = (long long)bc.i * W + bc.j;
                     }
@@ -534,17 +570,27 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     for (int v = 0; v < V; ++v) prevb[v] = Lr[v];
                     pminb = nmin;
                     bc.advance(W, D, WD);
-                    if (NEED_ACC) load_v<V>(ab[r], a.acc_in + pc.off + e0, active);
-                    if (NEED_S) load_v<V>(sb[r], a.s_in + pc.off + e0, active);
+                    if (NEED_ACC) load_v<V>(ab[q], a.acc_in + pc.off + e0, active);
+                    if (NEED_S) load_v<V>(sb[q], a.s_in + pc.off + e0, active);
                     pc.advance_upto(n, W, D, WD);
                 }
             }
             lds_barrier();
         };
+        using h0 = std::integral_constant<int, 0>;
+        using h1 = std::integral_constant<int, RH - 1>;
         lds_barrier();
         int c = 0;
-        for (; c < nseg - 1; ++c) consume(c, full_t{});
-        consume(nseg - 1, part_t{});
+        for (; c + RH <= nseg - 1; c += RH) {
+            consume(c, full_t{}, h0{});
+            if constexpr (RH == 2) consume(c + 1, full_t{}, h1{});
+        }
+        if (RH == 2 && c < nseg - 1) {
+            consume(c, full_t{}, h0{});
+            consume(c + 1, part_t{}, h1{});
+        } else {
+            consume(c, part_t{}, h0{});
+        }
         if (FINAL) lds_barrier();
     } else if constexpr (FINAL) {
         // ------------------------------------------------- WTA (wave 2)

@@ -94,14 +94,23 @@ hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64
 // ------------------------------------------------ DSI + horizontal IIR
 
 // One thread per (row, d) chain, R rows per block (R*D threads).  The census
-// rows of both images (and the sky row) are staged in LDS once per block; the
-// raw Hamming DSI (Solver.cpp:143-248, sky override :165-178) is produced on
-// the fly and fed straight into the in-place horizontal IIR of
-// Solver.cpp:296-330, restated with a register history: with h = WIN/2 and
-// LAG = WIN-h-1 the reference writes position LAG+t at step t, adds raw[WIN+t]
-// and subtracts the value at position t, which is the step-(t-LAG) output once
-// t >= LAG and raw before.
+// rows of both images (and the sky row) are staged in LDS once per block,
+// padded on both sides with copies of the edge words so the clamped lookups
+// of Solver.cpp:143-248 become plain offsets; the raw Hamming DSI (sky
+// override :165-178) is produced on the fly and fed straight into the
+// in-place horizontal IIR of Solver.cpp:296-330, restated with a register
+// history: with h = WIN/2 and LAG = WIN-h-1 the reference writes position
+// LAG+t at step t, adds raw[WIN+t] and subtracts the value at position t,
+// which is the step-(t-LAG) output once t >= LAG and raw before.
+//
+// The IIR is one serial chain per (row, d) and a frame has only H*D of them
+// (750 waves at KITTI D=128), so a wave's step latency is the kernel time:
+// the main loop runs blocks of COSTH_U steps with no branches, their raw
+// costs fetched one block ahead.
 constexpr int COSTH_MAX_LDS = 64 * 1024;
+constexpr int COSTH_U = 8;
+
+__host__ __device__ constexpr int costh_pad(int D, int scale) { return D / scale + 2 * COSTH_U; }
 
 template <int VIEW, int WIN, bool SKY, bool FILTER>
 __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
@@ -110,12 +119,14 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
                                                      int sky_pitch, int H, int W, int D, int scale,
                                                      int R, float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int P = costh_pad(D, scale), RS = W + 2 * P;
     uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
-    uint64_t *sr = sl + (size_t)R * W;
-    uint8_t *ss = reinterpret_cast<uint8_t *>(sr + (size_t)R * W);
+    uint64_t *sr = sl + (size_t)R * RS;
+    uint8_t *ss = reinterpret_cast<uint8_t *>(sr + (size_t)R * RS);
     const int row0 = blockIdx.x * R;
-    for (int idx = threadIdx.x; idx < R * W; idx += blockDim.x) {
-        const int r = idx / W, j = idx - r * W, i = row0 + r;
+    for (int idx = threadIdx.x; idx < R * RS; idx += blockDim.x) {
+        const int r = idx / RS, jp = idx - r * RS, i = row0 + r;
+        const int j = clampi(jp - P, 0, W - 1);
         if (i < H) {
             sl[idx] = ctl[(size_t)i * W + j];
             sr[idx] = ctr[(size_t)i * W + j];
@@ -126,23 +137,19 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     const int r = threadIdx.x / D, d = threadIdx.x - r * D;
     const int i = row0 + r;
     if (i >= H) return;
-    const uint64_t *cl = sl + (size_t)r * W;
-    const uint64_t *cr = sr + (size_t)r * W;
-    const uint8_t *sk = ss + (size_t)r * W;
     const int ds = d / scale;
+    // raw(j) reads cl[j (+ds)] and cr[j (-ds)] through the padded rows
+    const uint64_t *cl = sl + (size_t)r * RS + P + (VIEW == 1 ? ds : 0);
+    const uint64_t *cr = sr + (size_t)r * RS + P - (VIEW == 0 ? ds : 0);
+    const uint8_t *sk = ss + (size_t)r * RS + P;
     float *o = out + (size_t)i * W * D + d;
 
     auto raw = [&](int j) -> float {
-        uint64_t a, b;
-        if (VIEW == 0) {
-            a = cl[j];
-            b = cr[max(j - ds, 0)];
-        } else {
-            a = cl[min(j + ds, W - 1)];
-            b = cr[j];
+        const float c = hamming(cl[j], cr[j]);
+        if (SKY) {
+            const float sv = d == 0 ? 0.0f : 999999.0f;
+            return sk[j] == 255 ? sv : c;
         }
-        const float c = (float)__popcll(a ^ b);
-        if (SKY && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
         return c;
     };
 
@@ -150,29 +157,55 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
         for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
         return;
     }
-    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1;
+    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, U = COSTH_U;
     float sum = 0.0f;
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
 #pragma unroll
     for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
     const int T = W - 2 * HALF;
-    float o1 = 0.0f, o2 = 0.0f;
-    const float r0 = raw(0), r1 = raw(1);
-#pragma unroll 8
-    for (int t = 0; t < T; ++t) {
+    // hist[0] is what step t subtracts: raw[t] for t < LAG, output t-LAG after
+    float hist[LAG > 0 ? LAG : 1];
+#pragma unroll
+    for (int p = 0; p < LAG; ++p) hist[p] = raw(p);
+    auto step = [&](int t, float rw) {
         const float v = div_win<WIN>(sum);
         o[(size_t)(LAG + t) * D] = v;
-        if (t == T - 1) break;
-        sum += raw(WIN + t);
+        sum += rw;
         float a;
-        if (LAG == 0) a = v;
-        else if (LAG == 1) a = t >= 1 ? o1 : r0;
-        else a = t >= 2 ? o2 : (t == 0 ? r0 : r1);
+        if constexpr (LAG == 0) {
+            a = v;
+        } else {
+            a = hist[0];
+#pragma unroll
+            for (int p = 0; p + 1 < LAG; ++p) hist[p] = hist[p + 1];
+            hist[LAG - 1] = v;
+        }
         sum -= a;
-        o2 = o1;
-        o1 = v;
+    };
+    // steps t < T-1 also add raw[WIN+t]; the last step only writes
+    int t = 0;
+    float cur[U];
+    if (T - 1 >= U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = raw(WIN + u);
     }
+    for (; t + 2 * U <= T - 1; t += U) {
+        float nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = raw(WIN + t + U + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) step(t + u, cur[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+    if (t + U <= T - 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) step(t + u, cur[u]);
+        t += U;
+    }
+    for (; t < T - 1; ++t) step(t, raw(WIN + t));
+    if (T >= 1) o[(size_t)(LAG + T - 1) * D] = div_win<WIN>(sum);
     for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
 }
 
@@ -197,7 +230,7 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
         if (SKY && sk[j] == 255) return d == 0 ? 0.0f : 999999.0f;
         const uint64_t a = VIEW == 0 ? cl[j] : cl[min(j + ds, W - 1)];
         const uint64_t b = VIEW == 0 ? cr[max(j - ds, 0)] : cr[j];
-        return (float)__popcll(a ^ b);
+        return hamming(a, b);
     };
     if (!FILTER) {
         for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
@@ -230,7 +263,8 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
 template <int VIEW, int WIN, bool SKY, bool FILTER>
 static void launch_cost_h_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                             int sky_pitch, Geom g, float *out, hipStream_t st) {
-    const size_t row_bytes = (size_t)g.W * (16 + (SKY ? 1 : 0));
+    const size_t row_bytes =
+        (size_t)(g.W + 2 * costh_pad(g.D, g.scale)) * (16 + (SKY ? 1 : 0));
     int R = (int)(COSTH_MAX_LDS / row_bytes);
     if (R > 256 / g.D) R = 256 / g.D;
     if (R >= 1) {

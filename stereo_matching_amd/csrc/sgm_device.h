@@ -16,6 +16,14 @@ namespace sgm {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Hamming distance of two census words as an exact float.  Two 32-bit counts
+// (v_bcnt_u32_b32 accumulates) keep the conversion a single v_cvt_f32_i32;
+// a 64-bit popcount is converted through the u64 -> f32 sequence.
+__device__ __forceinline__ float hamming(uint64_t a, uint64_t b) {
+    const uint64_t x = a ^ b;
+    return (float)(int)(__builtin_popcount((uint32_t)x) + __builtin_popcount((uint32_t)(x >> 32)));
+}
+
 // DPP move with an explicit fill value for lanes whose source is invalid or
 // masked off (bound_ctrl = 0 keeps `old`).
 template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
@@ -322,6 +330,9 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    // keep the scheduler from hoisting work of the next segment (and the
+    // waits its loads need) above the barrier
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // Partial WTA state over a set of disparities: the minimum m and the first

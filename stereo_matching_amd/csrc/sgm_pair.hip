@@ -141,13 +141,15 @@ __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
 }
 
 // The final pass of a view: PAIR_V backward (L4, recomputing L3) summed with
-// S12 and T, then WTA.  Wave 0 produces total-cost rows into a double-buffered
-// LDS ring, wave 1 runs the batched WTA on the previous chunk.
+// S12 and T, then WTA.  Three waves (pair_split_body): wave 0 recomputes L3
+// segments from their checkpoints, wave 1 runs L4 and sums the totals into an
+// LDS ring, wave 2 runs the batched WTA on the chunk before.
 template <int V, bool FULL>
-__global__ __launch_bounds__(128) void pair_final_kernel(PairArgs a, Geom g) {
-    __shared__ __attribute__((aligned(16))) float tbuf[2][pair_kv<V>()][tbuf_stride<V>()];
-    __shared__ long long pbuf[2][pair_kv<V>()];
-    pair_bwd_body<PAIR_V, V, FULL, PAIR_FINAL>(a, g, blockIdx.x, tbuf, pbuf);
+__global__ __launch_bounds__(192) void pair_final_kernel(PairArgs a, Geom g) {
+    constexpr int K = pair_kv<V>();
+    __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
+    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2>(a, g, blockIdx.x, threadIdx.x >> 6, lds.s,
+                                                    &lds);
 }
 
 // Multi-role stage kernels of the frame schedule: block ranges run different
@@ -173,11 +175,20 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
     pair_fwd_body<5, V, FULL, PFD>(d6, g, b - g.W);
 }
 
+// Stage B blocks are two waves: an H block splits its row's L2 pass into a
+// recompute wave and a backward wave (pair_split_body); a D2 block runs two
+// anti-diagonal L7 chains, one per wave.
 template <int V, bool FULL>
-__global__ __launch_bounds__(64) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
-    const int b = blockIdx.x;
-    if (b < g.H) pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, b, nullptr, nullptr);
-    else pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(d7, g, b - g.H, nullptr, nullptr);
+__global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
+    constexpr int K = pair_k<V>();
+    __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
+    const int b = blockIdx.x, wave = threadIdx.x >> 6;
+    if (b < g.H) {
+        pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K>(h2, g, b, wave, lds, nullptr);
+        return;
+    }
+    const int path = 2 * (b - g.H) + wave;
+    if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(d7, g, path, nullptr, nullptr);
 }
 
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
@@ -191,11 +202,11 @@ hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArg
 }
 
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st) {
-    const dim3 grid(g.H + g.W);
-    if (g.D == 32) stage_b_kernel<1, false><<<grid, 64, 0, st>>>(h2, d7, g);
-    else if (g.D == 64) stage_b_kernel<1, true><<<grid, 64, 0, st>>>(h2, d7, g);
-    else if (g.D == 128) stage_b_kernel<2, true><<<grid, 64, 0, st>>>(h2, d7, g);
-    else stage_b_kernel<4, true><<<grid, 64, 0, st>>>(h2, d7, g);
+    const dim3 grid(g.H + (g.W + 1) / 2);
+    if (g.D == 32) stage_b_kernel<1, false><<<grid, 128, 0, st>>>(h2, d7, g);
+    else if (g.D == 64) stage_b_kernel<1, true><<<grid, 128, 0, st>>>(h2, d7, g);
+    else if (g.D == 128) stage_b_kernel<2, true><<<grid, 128, 0, st>>>(h2, d7, g);
+    else stage_b_kernel<4, true><<<grid, 128, 0, st>>>(h2, d7, g);
     return hipGetLastError();
 }
 
@@ -246,10 +257,10 @@ static void launch_bwd_t(const PairArgs &a, Geom g, hipStream_t st) {
 
 static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(g.W);
-    if (g.D == 32) pair_final_kernel<1, false><<<grid, 128, 0, st>>>(a, g);
-    else if (g.D == 64) pair_final_kernel<1, true><<<grid, 128, 0, st>>>(a, g);
-    else if (g.D == 128) pair_final_kernel<2, true><<<grid, 128, 0, st>>>(a, g);
-    else pair_final_kernel<4, true><<<grid, 128, 0, st>>>(a, g);
+    if (g.D == 32) pair_final_kernel<1, false><<<grid, 192, 0, st>>>(a, g);
+    else if (g.D == 64) pair_final_kernel<1, true><<<grid, 192, 0, st>>>(a, g);
+    else if (g.D == 128) pair_final_kernel<2, true><<<grid, 192, 0, st>>>(a, g);
+    else pair_final_kernel<4, true><<<grid, 192, 0, st>>>(a, g);
 }
 
 hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipStream_t st) {

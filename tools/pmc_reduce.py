@@ -1,0 +1,67 @@
+"""Reduce rocprofv3 FETCH_SIZE / WRITE_SIZE passes to bytes per launch.
+
+FETCH_SIZE and WRITE_SIZE are reported in KiB.  On gfx950 FETCH_SIZE counts
+wide coalesced streaming reads at half their bytes (MI355X_MICROARCH.md,
+"HBM"), so it is doubled; WRITE_SIZE is exact for streaming stores.
+Usage: python tools/pmc_reduce.py TAG CONFIG  (after tools/pmc.sh)
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# kernel symbol -> name used by the library's in-process profiler (bench.py)
+NAMES = [("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
+         ("pair_final_kernel", "pair_bwd_L4_final"), ("vfwd_kernel", "vfwd"),
+         ("cost_h_kernel", "cost_h"), ("cost_h_global_kernel", "cost_h"),
+         ("census_kernel", "census"), ("lr_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc")]
+
+
+def short(name):
+    for key, val in NAMES:
+        if key in name:
+            return val
+    return None
+
+
+def per_launch(tag, counter):
+    files = glob.glob(os.path.join(ROOT, "gpurun_out", f"{tag}_pmc_{counter}", "**",
+                                   "*counter_collection.csv"), recursive=True)
+    acc = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            k = short(row.get("Kernel_Name", ""))
+            if k and row.get("Counter_Name") == counter:
+                acc[k].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    tag, cfg = sys.argv[1], sys.argv[2]
+    fetch = per_launch(tag, "FETCH_SIZE")
+    write = per_launch(tag, "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        rd = 2.0 * fetch.get(k, 0.0) * 1024.0
+        wr = write.get(k, 0.0) * 1024.0
+        out[k] = {"read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    data = {}
+    if os.path.exists(path):
+        data = json.load(open(path))
+    data[cfg] = {k: v["bytes"] for k, v in out.items()}
+    data.setdefault("_detail", {})[cfg] = out
+    data["_source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, tag {tag}; "
+                       "FETCH_SIZE doubled (gfx950), KiB -> bytes; per-launch means")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    json.dump(data, open(path, "w"), indent=1, sort_keys=True)
+    for k, v in out.items():
+        print(f"  {k:22s} read {v['read_bytes']/1e6:9.1f} MB  write {v['write_bytes']/1e6:9.1f} MB")
+
+
+if __name__ == "__main__":
+    main()
