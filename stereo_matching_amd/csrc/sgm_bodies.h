@@ -38,7 +38,7 @@ __device__ __forceinline__ float lane_min(const float (&x)[V]) {
 template <int DIR, int V, int MODE, bool FULL, int PF>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, int path) {
     static_assert(MODE != SWEEP_FINAL, "the final pass is pair_final_kernel");
-    const int lane = threadIdx.x & 63;
+    const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
     const int n = DIR < 2 ? W : H;
@@ -137,7 +137,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 template <int FD, int V, bool FULL, int PF>
 __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, int path) {
     constexpr int K = family_k<FD == 0 ? PAIR_H : (FD == 2 ? PAIR_V : PAIR_D2), V>();
-    const int lane = threadIdx.x & 63;
+    const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
     const int n = FD == 0 ? W : H;
@@ -207,8 +207,8 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     constexpr bool FINAL = MODE == PAIR_FINAL;
     constexpr bool NEED_ACC = MODE != PAIR_INIT2;
     constexpr bool NEED_S = FINAL;
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
+    const int wave = wave_id();
+    const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
     const int n = FAM == PAIR_H ? W : H;
@@ -409,7 +409,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     constexpr int NW = FINAL ? 3 : 2;
     constexpr bool NEED_ACC = MODE != PAIR_INIT2;
     constexpr bool NEED_S = FINAL;
-    const int lane = threadIdx.x & 63;
+    const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
     const int n = FAM == PAIR_H ? W : H;

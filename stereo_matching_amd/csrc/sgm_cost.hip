@@ -56,16 +56,16 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
                                                      uint64_t *__restrict__ ct) {
     constexpr int TR = CT_TH + 2 * HH, TC = CT_TW + 2 * HWW;
     __shared__ uint8_t tile[TR][TC];
-    const int x0 = blockIdx.x * CT_TW, y0 = blockIdx.y * CT_TH;
-    for (int idx = threadIdx.x; idx < TR * TC; idx += 256) {
+    const int x0 = bid_x() * CT_TW, y0 = bid_y() * CT_TH;
+    for (int idx = tid_x(); idx < TR * TC; idx += 256) {
         const int ty = idx / TC, tx = idx - ty * TC;
         const int y = clampi(y0 + ty - HH, 0, H - 1), x = clampi(x0 + tx - HWW, 0, W - 1);
         tile[ty][tx] = blur ? (uint8_t)blur_at(src, pitch, step, H, W, y, x)
                             : src[(size_t)y * step * pitch + (size_t)x * step];
     }
     __syncthreads();
-    const int tx = threadIdx.x & 63;
-    for (int r = threadIdx.x >> 6; r < CT_TH; r += 4) {
+    const int tx = tid_x() & 63;
+    for (int r = wave_id(); r < CT_TH; r += 4) {
         const int y = y0 + r, x = x0 + tx;
         if (y >= H || x >= W) continue;
         const uint8_t c = tile[r + HH][tx + HWW];
@@ -123,8 +123,8 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
     uint64_t *sr = sl + (size_t)R * RS;
     uint8_t *ss = reinterpret_cast<uint8_t *>(sr + (size_t)R * RS);
-    const int row0 = blockIdx.x * R;
-    for (int idx = threadIdx.x; idx < R * RS; idx += blockDim.x) {
+    const int row0 = bid_x() * R;
+    for (int idx = tid_x(); idx < R * RS; idx += R * D) {
         const int r = idx / RS, jp = idx - r * RS, i = row0 + r;
         const int j = clampi(jp - P, 0, W - 1);
         if (i < H) {
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
         }
     }
     __syncthreads();
-    const int r = threadIdx.x / D, d = threadIdx.x - r * D;
+    const int r = tid_x() / D, d = tid_x() - r * D;
     const int i = row0 + r;
     if (i >= H) return;
     const int ds = d / scale;
@@ -218,8 +218,8 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
                                                             int sky_pitch, int H, int W, int D,
                                                             int scale, float *__restrict__ out) {
     const int rows_per_block = 256 / D;
-    const int r = threadIdx.x / D, d = threadIdx.x - r * D;
-    const int i = blockIdx.x * rows_per_block + r;
+    const int r = tid_x() / D, d = tid_x() - r * D;
+    const int i = bid_x() * rows_per_block + r;
     if (i >= H) return;
     const uint64_t *cl = ctl + (size_t)i * W;
     const uint64_t *cr = ctr + (size_t)i * W;
@@ -309,7 +309,7 @@ hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t
 // sgm_pair.hip (vfwd_kernel); without the filter the volume is copied.
 __global__ __launch_bounds__(256) void copy_kernel(const float *__restrict__ in,
                                                    float *__restrict__ out, size_t n) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t i = (size_t)bid_x() * 256 + tid_x();
     if (i < n) out[i] = in[i];
 }
 

@@ -14,6 +14,18 @@ namespace sgm {
 
 // ---------------------------------------------------------------- helpers
 
+// Work-item / workgroup ids straight from the hardware registers.  blockIdx /
+// threadIdx go through the device library (__ockl_get_group_id, ...), which
+// is compiled without -mno-amdgpu-ieee and therefore never inlined into these
+// kernels: every id would come back from a call, in a VGPR, and everything
+// derived from it (scanline cursors, addresses) would run on the VALU.
+__device__ __forceinline__ int bid_x() { return (int)__builtin_amdgcn_workgroup_id_x(); }
+__device__ __forceinline__ int bid_y() { return (int)__builtin_amdgcn_workgroup_id_y(); }
+__device__ __forceinline__ int tid_x() { return (int)__builtin_amdgcn_workitem_id_x(); }
+// index of the calling wave in its workgroup, as a scalar (role dispatch on it
+// must be a uniform branch, not an exec-masked one)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(tid_x() >> 6); }
+
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // Hamming distance of two census words as an exact float.  Two 32-bit counts

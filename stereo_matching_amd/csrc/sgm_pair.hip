@@ -43,8 +43,8 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
                                                   float *__restrict__ out, PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, LA = HALF + 1;
-    const int lane = threadIdx.x;
-    const int j = blockIdx.x;
+    const int lane = tid_x();
+    const int j = bid_x();
     const int H = g.H;
     const size_t stride = (size_t)g.W * g.D;
     const int e0 = lane * V;
@@ -132,12 +132,12 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
 
 template <int FD, int V, bool FULL, int PF>
 __global__ __launch_bounds__(64) void pair_fwd_kernel(PairArgs a, Geom g) {
-    pair_fwd_body<FD, V, FULL, PF>(a, g, blockIdx.x);
+    pair_fwd_body<FD, V, FULL, PF>(a, g, bid_x());
 }
 
 template <int FAM, int V, bool FULL, int MODE>
 __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
-    pair_bwd_body<FAM, V, FULL, MODE>(a, g, blockIdx.x, nullptr, nullptr);
+    pair_bwd_body<FAM, V, FULL, MODE>(a, g, bid_x(), nullptr, nullptr);
 }
 
 // The final pass of a view: PAIR_V backward (L4, recomputing L3) summed with
@@ -148,7 +148,7 @@ template <int V, bool FULL>
 __global__ __launch_bounds__(192) void pair_final_kernel(PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
     __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
-    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2>(a, g, blockIdx.x, threadIdx.x >> 6, lds.s,
+    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2>(a, g, bid_x(), wave_id(), lds.s,
                                                     &lds);
 }
 
@@ -162,7 +162,7 @@ template <int V, bool FULL>
 __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, PairArgs d6,
                                                      Geom g) {
     constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
-    int b = blockIdx.x;
+    int b = bid_x();
     if (b < g.H) {
         pair_fwd_body<0, V, FULL, PFH>(h1, g, b);
         return;
@@ -182,7 +182,7 @@ template <int V, bool FULL>
 __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
     constexpr int K = pair_k<V>();
     __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
-    const int b = blockIdx.x, wave = threadIdx.x >> 6;
+    const int b = bid_x(), wave = wave_id();
     if (b < g.H) {
         pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K>(h2, g, b, wave, lds, nullptr);
         return;

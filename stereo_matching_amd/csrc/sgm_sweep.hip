@@ -21,7 +21,7 @@ namespace sgm {
 
 template <int DIR, int V, int MODE, bool FULL, int PF>
 __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
-    sweep_body<DIR, V, MODE, FULL, PF>(a, g, blockIdx.x);
+    sweep_body<DIR, V, MODE, FULL, PF>(a, g, bid_x());
 }
 
 // Steps of loads kept in flight: horizontal paths (few, long, latency-bound)
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void lr_kernel(const float *__restrict__ fl,
                                                  const float *__restrict__ fr,
                                                  float *__restrict__ out, int out_pitch, int H,
                                                  int W, int D, int scale, float lr) {
-    const int j = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y;
+    const int j = bid_x() * 256 + tid_x(), i = bid_y();
     if (j >= W) return;
     float dl = fl[(size_t)i * W + j];
     if (j >= dl) {

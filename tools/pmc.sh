@@ -13,4 +13,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     -- python bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass \
     > gpurun_out/${TAG}_pmc_${C}.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_${C}.log; exit 1; }
 done
-python tools/pmc_reduce.py "$TAG" "$CFG"
+python tools/pmc_reduce.py "$TAG" "$CFG" && cp profiles/pmc_traffic.json gpurun_out/${TAG}_pmc_traffic.json
