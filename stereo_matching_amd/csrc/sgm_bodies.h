@@ -35,9 +35,25 @@ __device__ __forceinline__ float lane_min(const float (&x)[V]) {
 // lanes 0..31 and +inf above).  Loads run PF steps ahead of the DP through a
 // register ring.  Modes STORE_L / INIT / ACC (the final sweep has its own
 // two-wave kernel).
+#ifdef SGM_STAMPS
+// per role (0-2 final producer/consumer/WTA, 3-4 H producer/consumer):
+// work cycles, barrier-wait cycles, waves
+static __device__ unsigned long long sgm_stamps[16][3];  // one copy per translation unit
+__device__ __forceinline__ void stamp_flush(int role, long long t0) {
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if ((tid_x() & 63) == 0) {
+        atomicAdd(&sgm_stamps[role][0], (unsigned long long)(t1 - t0));
+        atomicAdd(&sgm_stamps[role][2], 1ull);
+    }
+}
+#endif
+
 template <int DIR, int V, int MODE, bool FULL, int PF>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, int path) {
     static_assert(MODE != SWEEP_FINAL, "the final pass is pair_final_kernel");
+#ifdef SGM_STAMPS
+    const long long st_t0 = __builtin_amdgcn_s_memtime();
+#endif
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -114,6 +130,9 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 #pragma unroll
     for (int u = 0; u < PF; ++u)
         if (k0 + u < n) step(u, false);
+#ifdef SGM_STAMPS
+    stamp_flush(DIR == 4 ? 8 : (DIR == 7 ? 9 : 10), st_t0);
+#endif
 }
 
 // --------------------------------------------------------------- pairs
@@ -136,6 +155,9 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 // output is the checkpoint set.
 template <int FD, int V, bool FULL, int PF>
 __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, int path) {
+#ifdef SGM_STAMPS
+    const long long st_t0 = __builtin_amdgcn_s_memtime();
+#endif
     constexpr int K = family_k<FD == 0 ? PAIR_H : (FD == 2 ? PAIR_V : PAIR_D2), V>();
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
@@ -191,6 +213,9 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
 #pragma unroll
     for (int u = 0; u < PF; ++u)
         if (k0 + u < n) step(u, false);
+#ifdef SGM_STAMPS
+    stamp_flush(FD == 0 ? 5 : (FD == 5 ? 6 : 7), st_t0);
+#endif
 }
 
 // ------------------------------------------------------- backward pass
@@ -201,6 +226,9 @@ template <int FAM, int V, bool FULL, int MODE>
 __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, int path,
                                               float (*tb)[family_k<FAM, V>()][tbuf_stride<V>()],
                                               long long (*pb)[family_k<FAM, V>()]) {
+#ifdef SGM_STAMPS
+    const long long st_t0 = __builtin_amdgcn_s_memtime();
+#endif
     constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
     constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
     constexpr int K = family_k<FAM, V>();
@@ -366,6 +394,9 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
         process_seg(c0, 0, part_t{});
     }
     if (FINAL) lds_barrier();
+#ifdef SGM_STAMPS
+    stamp_flush(FAM == PAIR_D2 ? 11 : (FAM == PAIR_H ? 13 : 14), st_t0);
+#endif
 }
 
 // ------------------------------------------------- split pair backward
@@ -381,6 +412,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
 // Barrier schedule (every wave runs nseg + NW - 1 LDS barriers): in
 // iteration t the producer fills chunk t, the consumer drains chunk t-1 and
 // the WTA wave chunk t-2 (chunk c = segment nseg-1-c).
+
 template <int K, int V>
 struct SplitLds {
     float c[2][K][tbuf_stride<V>()];    // segment costs
@@ -401,6 +433,20 @@ template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1>
 __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g, int path,
                                                 int wave, SplitLds<K, V> &L,
                                                 SplitFinalLds<K, V> *F) {
+#ifdef SGM_STAMPS
+    long long st_prev = __builtin_amdgcn_s_memtime(), st_work = 0, st_wait = 0;
+    auto bar = [&] {
+        const long long t0 = __builtin_amdgcn_s_memtime();
+        lds_barrier();
+        const long long t1 = __builtin_amdgcn_s_memtime();
+        st_work += t0 - st_prev;
+        st_wait += t1 - t0;
+        st_prev = t1;
+    };
+#else
+    auto bar = [] { lds_barrier(); };
+#endif
+
     static_assert(NB == 2 || NB == 3, "producer buffers");
     static_assert(RH == 1 || RH == 2, "consumer ring halves");
     constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
@@ -421,6 +467,8 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     using part_t = std::integral_constant<bool, false>;
 
     if (wave == 0) {
+        // H rows: the recompute chain is the slower one; V: the backward one
+        __builtin_amdgcn_s_setprio(FAM == PAIR_H ? 3 : 2);
         // ---------------------------------------------------- producer
         const float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
         float cb[NB][K + 1][V];
@@ -476,7 +524,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     fc.advance(W, D, WD);
                 }
             }
-            lds_barrier();
+            bar();
         };
         // buffer u holds segment nseg-1-m for m = u (mod NB)
 #pragma unroll
@@ -510,8 +558,10 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         else if (b0 == 1) produce(cb[1], 0, part_t{});
         else produce(cb[NB - 1], 0, part_t{});
 #pragma unroll
-        for (int t = 0; t < NW - 1; ++t) lds_barrier();
+        for (int t = 0; t < NW - 1; ++t) bar();
     } else if (wave == 1) {
+        // the backward chain is the critical path of the pair: issue priority
+        __builtin_amdgcn_s_setprio(3);
         // ---------------------------------------------------- consumer
         constexpr int RD = RH * K;
         const int bpath = FAM == PAIR_D2 ? uniform(((path - (H - 1)) % W + W) % W) : path;
@@ -575,11 +625,11 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     pc.advance_upto(n, W, D, WD);
                 }
             }
-            lds_barrier();
+            bar();
         };
         using h0 = std::integral_constant<int, 0>;
         using h1 = std::integral_constant<int, RH - 1>;
-        lds_barrier();
+        bar();
         int c = 0;
         for (; c + RH <= nseg - 1; c += RH) {
             consume(c, full_t{}, h0{});
@@ -591,17 +641,26 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         } else {
             consume(c, part_t{}, h0{});
         }
-        if (FINAL) lds_barrier();
+        if (FINAL) bar();
     } else if constexpr (FINAL) {
+        __builtin_amdgcn_s_setprio(1);
         // ------------------------------------------------- WTA (wave 2)
-        lds_barrier();
-        lds_barrier();
+        bar();
+        bar();
         for (int c = 0; c < nseg; ++c) {
             wta_consume_chunk<V, K>(F->t[c & 1], F->p[c & 1], c == nseg - 1 ? r0 : K, lane, g.D,
                                     a.uniq, a.disp, a.sub);
-            lds_barrier();
+            bar();
         }
     }
+#ifdef SGM_STAMPS
+    if (lane == 0) {
+        const int role = wave + (FAM == PAIR_V ? 0 : 3);
+        atomicAdd(&sgm_stamps[role][0], (unsigned long long)st_work);
+        atomicAdd(&sgm_stamps[role][1], (unsigned long long)st_wait);
+        atomicAdd(&sgm_stamps[role][2], 1ull);
+    }
+#endif
 }
 
 }  // namespace sgm

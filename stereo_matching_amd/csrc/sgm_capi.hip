@@ -47,6 +47,8 @@ struct sgm_handle {
     float *d_out;         // LR-checked output (host API)
     float *d_min;         // minL (stage_path)
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
+    uint8_t *h_pin;       // pinned host staging for sgm_process (allocated on first use)
+    size_t h_pin_bytes;
     char err[512];
     // profiling (sgm_set_profiling)
     int profiling;
@@ -125,6 +127,8 @@ void free_all(sgm_handle *h) {
     }
     (void)hipFree(h->d_out);
     (void)hipFree(h->d_min);
+    if (h->h_pin) (void)hipHostFree(h->h_pin);
+    h->h_pin = nullptr;
     for (auto &v : h->d_ck)
         for (auto p : v) (void)hipFree(p);
     if (h->st) (void)hipStreamDestroy(h->st);
@@ -319,16 +323,33 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     return SGM_OK;
 }
 
+// Pinned staging for the host-buffer API: user rows are packed into pinned
+// memory on the CPU, so every host<->device transfer is one contiguous DMA
+// (pageable 2-D copies went through the runtime's staging path at a fraction
+// of PCIe bandwidth).  Layout: left | right | sky_l | sky_r | out f32 | raw u16.
+int ensure_pinned(sgm_handle *h) {
+    const size_t nin = (size_t)h->p.height * h->p.width, npx = (size_t)h->g.H * h->g.W;
+    const size_t need = 2 * nin + 2 * npx + npx * sizeof(float) + npx * sizeof(uint16_t) + 64;
+    if (h->h_pin && h->h_pin_bytes >= need) return SGM_OK;
+    if (h->h_pin) (void)hipHostFree(h->h_pin);
+    h->h_pin = nullptr;
+    HIPCHK(h, hipHostMalloc((void **)&h->h_pin, need, hipHostMallocDefault));
+    h->h_pin_bytes = need;
+    return SGM_OK;
+}
+
 int copy_in_image(sgm_handle *h, uint8_t *dst, const uint8_t *src, int pitch) {
     HIPCHK(h, hipMemcpy2DAsync(dst, (size_t)h->p.width, src, (size_t)pitch, (size_t)h->p.width,
                                (size_t)h->p.height, hipMemcpyHostToDevice, h->st));
     return SGM_OK;
 }
 
-int copy_in_mask(sgm_handle *h, uint8_t *dst, const uint8_t *src, int pitch) {
-    HIPCHK(h, hipMemcpy2DAsync(dst, (size_t)h->g.W, src, (size_t)pitch, (size_t)h->g.W,
-                               (size_t)h->g.H, hipMemcpyHostToDevice, h->st));
-    return SGM_OK;
+void pack_rows(uint8_t *dst, const uint8_t *src, size_t row_bytes, int rows, size_t pitch) {
+    if (pitch == row_bytes) {
+        memcpy(dst, src, row_bytes * rows);
+        return;
+    }
+    for (int i = 0; i < rows; ++i) memcpy(dst + i * row_bytes, src + i * pitch, row_bytes);
 }
 
 }  // namespace
@@ -466,22 +487,34 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: bad pointer or pitch");
     DeviceGuard guard(h->device);
     int rc;
-    if ((rc = copy_in_image(h, h->d_in[0], left, pitch))) return rc;
-    if ((rc = copy_in_image(h, h->d_in[1], right, pitch))) return rc;
-    if (sky_l && (rc = copy_in_mask(h, h->d_sky[0], sky_l, sky_pitch))) return rc;
-    if (sky_r && (rc = copy_in_mask(h, h->d_sky[1], sky_r, sky_pitch))) return rc;
-    uint16_t *d_raw = raw_disp ? h->d_disp[0] : nullptr;  // read back below
+    if ((rc = ensure_pinned(h))) return rc;
+    const size_t nin = (size_t)h->p.height * h->p.width, npx = (size_t)h->g.H * h->g.W;
+    uint8_t *pl = h->h_pin, *pr = pl + nin, *psl = pr + nin, *psr = psl + npx;
+    float *pout = reinterpret_cast<float *>(psr + npx + (16 - (size_t)(psr + npx) % 16) % 16);
+    uint16_t *praw = reinterpret_cast<uint16_t *>(pout + npx);
+    pack_rows(pl, left, h->p.width, h->p.height, pitch);
+    pack_rows(pr, right, h->p.width, h->p.height, pitch);
+    HIPCHK(h, hipMemcpyAsync(h->d_in[0], pl, nin, hipMemcpyHostToDevice, h->st));
+    HIPCHK(h, hipMemcpyAsync(h->d_in[1], pr, nin, hipMemcpyHostToDevice, h->st));
+    if (sky_l) {
+        pack_rows(psl, sky_l, h->g.W, h->g.H, sky_pitch);
+        HIPCHK(h, hipMemcpyAsync(h->d_sky[0], psl, npx, hipMemcpyHostToDevice, h->st));
+    }
+    if (sky_r) {
+        pack_rows(psr, sky_r, h->g.W, h->g.H, sky_pitch);
+        HIPCHK(h, hipMemcpyAsync(h->d_sky[1], psr, npx, hipMemcpyHostToDevice, h->st));
+    }
     if ((rc = run_frame(h, h->d_in[0], h->d_in[1], h->p.width, sky_l ? h->d_sky[0] : nullptr,
                         sky_r ? h->d_sky[1] : nullptr, h->g.W, h->d_out, h->g.W, nullptr, h->st)))
         return rc;
-    (void)d_raw;
-    HIPCHK(h, hipMemcpy2DAsync(out, (size_t)out_pitch * sizeof(float), h->d_out,
-                               (size_t)h->g.W * sizeof(float), (size_t)h->g.W * sizeof(float),
-                               h->g.H, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipMemcpyAsync(pout, h->d_out, npx * sizeof(float), hipMemcpyDeviceToHost, h->st));
     if (raw_disp)
-        HIPCHK(h, hipMemcpyAsync(raw_disp, h->d_disp[0], (size_t)h->g.H * h->g.W * sizeof(uint16_t),
-                                 hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipMemcpyAsync(praw, h->d_disp[0], npx * sizeof(uint16_t), hipMemcpyDeviceToHost,
+                                 h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
+    for (int i = 0; i < h->g.H; ++i)
+        memcpy(out + (size_t)i * out_pitch, pout + (size_t)i * h->g.W, h->g.W * sizeof(float));
+    if (raw_disp) memcpy(raw_disp, praw, npx * sizeof(uint16_t));
     return SGM_OK;
 }
 

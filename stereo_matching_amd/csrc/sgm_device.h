@@ -70,26 +70,43 @@ __device__ __forceinline__ float movdppf(float src) {
     return __int_as_float(movdpp<CTRL, ROW_MASK, BANK_MASK>(__float_as_int(src)));
 }
 
-// Minimum over the 64 lanes, left in EVERY lane (a VGPR, no readlane on the
-// DP chain): the quad, half-row and row mirrors give each lane its row (16
-// lane) minimum; v_permlane16_swap pairs rows 0<->1 and 2<->3, and
-// v_permlane32_swap the two wave halves (gfx950).
+// Minimum over the 64 lanes as a wave-uniform value (an SGPR, usable as the
+// scalar operand of the next step's VALU ops): quad, half-row and row mirrors
+// give every lane its 16-lane row minimum; row_bcast:15 folds row 0 into 1
+// and 2 into 3, row_bcast:31 folds lane 31 into rows 2-3, so lane 63 holds
+// the minimum (GFX9 DPP, valid on gfx950).  The row_bcast steps keep the
+// unmasked rows' values, which the compiler cannot express as a fused
+// v_min_f32_dpp, hence the inline asm; the s_nop covers the VALU-write ->
+// DPP-read hazard the hazard recognizer does not see inside asm.
 __device__ __forceinline__ float wave_min(float x) {
     x = fminf(x, movdppf<DPP_QP_1032>(x));
     x = fminf(x, movdppf<DPP_QP_2301>(x));
     x = fminf(x, movdppf<DPP_HALF_MIRROR>(x));
     x = fminf(x, movdppf<DPP_MIRROR>(x));
-    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x),
-                                                    false, false);
-    x = fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x),
-                                                    false, false);
-    return fminf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+    asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(x));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
 
-// Same, returned as a wave-uniform scalar.
-__device__ __forceinline__ float wave_min_u(float x) {
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_min(x))));
+// Same value (kept for call sites that want the name).
+__device__ __forceinline__ float wave_min_u(float x) { return wave_min(x); }
+
+// min(src of the neighbouring lane, a): SHR reads lane l-1, SHL lane l+1.
+// The edge lane (0 for SHR, 63 for SHL) has no source: with bound_ctrl off
+// the DPP op is disabled there and the tied destination keeps a.
+template <int CTRL>
+__device__ __forceinline__ float nbmin(float src, float a) {
+    float d = a;
+    if constexpr (CTRL == DPP_WAVE_SHR1)
+        asm("s_nop 1\n\tv_min_f32_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf"
+            : "+v"(d)
+            : "v"(src));
+    else
+        asm("s_nop 1\n\tv_min_f32_dpp %0, %1, %0 wave_shl:1 row_mask:0xf bank_mask:0xf"
+            : "+v"(d)
+            : "v"(src));
+    return d;
 }
 
 __device__ __forceinline__ int wave_min_i(int x) {
@@ -263,16 +280,36 @@ __device__ __forceinline__ void store_v(float *p, const float (&v)[V], bool acti
 template <int V>
 __device__ __forceinline__ void dp_step(const float (&prev)[V], float pmin, const float (&c)[V],
                                         float (&L)[V], float p1, float p2) {
-    const float left = dppf<DPP_WAVE_SHR1>(SGM_INF, prev[V - 1]);
-    const float right = dppf<DPP_WAVE_SHL1>(SGM_INF, prev[0]);
-    const float pmin_p2 = pmin + p2;
+    // neighbour minima min(L[d-1], L[d+1]); d = lane*V + v
+    float nb[V];
+    if constexpr (V == 1) {
+        const float right = dppf<DPP_WAVE_SHL1>(SGM_INF, prev[0]);
+        nb[0] = nbmin<DPP_WAVE_SHR1>(prev[0], right);
+    } else {
+        nb[0] = nbmin<DPP_WAVE_SHR1>(prev[V - 1], prev[1]);
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-        const float dm = v == 0 ? left : prev[v - 1];
-        const float dp = v == V - 1 ? right : prev[v + 1];
-        const float t = fminf(dm, dp) + p1;
-        const float m = fminf(fminf(prev[v], t), pmin_p2);
-        L[v] = m + (c[v] - pmin);
+        for (int v = 1; v < V - 1; ++v) nb[v] = fminf(prev[v - 1], prev[v + 1]);
+        nb[V - 1] = nbmin<DPP_WAVE_SHL1>(prev[0], prev[V - 2]);
+    }
+    const float pmin_p2 = pmin + p2;
+    if constexpr (V == 1) {
+        const float m = fminf(fminf(prev[0], nb[0] + p1), pmin_p2);
+        L[0] = m + (c[0] - pmin);
+    } else {
+        // pairs of lanes' values through packed f32 adds (v_pk_add_f32);
+        // same IEEE single additions as the scalar form
+        typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int v = 0; v < V; v += 2) {
+            const f2 t = f2{nb[v], nb[v + 1]} + p1;
+            const f2 d = f2{c[v], c[v + 1]} - pmin;
+            f2 m;
+            m.x = fminf(fminf(prev[v], t.x), pmin_p2);
+            m.y = fminf(fminf(prev[v + 1], t.y), pmin_p2);
+            const f2 r = m + d;
+            L[v] = r.x;
+            L[v + 1] = r.y;
+        }
     }
 }
 

@@ -18,6 +18,7 @@
 
 namespace sgm {
 
+
 static inline int vals_per_lane(int D) { return D >= 256 ? 4 : (D >= 128 ? 2 : 1); }
 static inline int chain_len(int family, Geom g) { return family == PAIR_H ? g.W : g.H; }
 static inline int num_chains(int family, Geom g) { return family == PAIR_H ? g.H : g.W; }
@@ -164,6 +165,8 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
     constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
     int b = bid_x();
     if (b < g.H) {
+        // the H chains (few, long) are the launch's critical path
+        __builtin_amdgcn_s_setprio(3);
         pair_fwd_body<0, V, FULL, PFH>(h1, g, b);
         return;
     }
@@ -184,7 +187,7 @@ __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, 
     __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
     const int b = bid_x(), wave = wave_id();
     if (b < g.H) {
-        pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K>(h2, g, b, wave, lds, nullptr);
+        pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K, 3>(h2, g, b, wave, lds, nullptr);
         return;
     }
     const int path = 2 * (b - g.H) + wave;
@@ -273,3 +276,15 @@ hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipS
 }
 
 }  // namespace sgm
+
+#ifdef SGM_STAMPS
+extern "C" int sgm_debug_stamps_pair(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sgm::sgm_stamps), sizeof(sgm::sgm_stamps)) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[16][3] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(sgm::sgm_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -94,3 +94,15 @@ hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch
 }
 
 }  // namespace sgm
+
+#ifdef SGM_STAMPS
+extern "C" int sgm_debug_stamps_sweep(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sgm::sgm_stamps), sizeof(sgm::sgm_stamps)) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[16][3] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(sgm::sgm_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

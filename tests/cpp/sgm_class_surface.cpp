@@ -1,0 +1,60 @@
+// Drives the reference's class surface (include/sgm_amd/SGM.h) the way the
+// ROS node does (node.cpp:49,93,104,107): construct SGM(h, w, s, d), process
+// a pair, read get_disp().
+//   sgm_class_surface nodevice            -> argument asserts + no-device error
+//   sgm_class_surface run L R H W D OUT   -> raw u8 pair in, f32 disparity out
+#define SGM_AMD_THROW 1
+#include "sgm_amd/SGM.h"
+
+#include <cstdio>
+#include <fstream>
+#include <vector>
+
+using sgm_amd::Mat;
+
+static int expect_throw(int h, int w, int s, int d) {
+    try {
+        sgm_amd::SGM sgm(h, w, s, d);
+    } catch (const std::runtime_error &e) {
+        std::printf("threw as expected (%d,%d,%d,%d): %s\n", h, w, s, d, e.what());
+        return 0;
+    }
+    std::printf("did not throw (%d,%d,%d,%d)\n", h, w, s, d);
+    return 1;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && std::string(argv[1]) == "nodevice") {
+        int bad = 0;
+        bad += expect_throw(375, 1242, 3, 128);  // s not in {1,2}   (Solver.cpp:8)
+        bad += expect_throw(375, 1242, 1, 48);   // d not allowed    (Solver.cpp:10)
+        bad += expect_throw(0, 1242, 1, 64);     // h > 0            (Solver.cpp:6)
+        bad += expect_throw(375, 1242, 1, 64);   // valid, but no GPU in this container
+        Mat m(4, 5, CV_32FC1);
+        m.at<float>(3, 4) = 2.5f;
+        Mat shallow = m;
+        bad += shallow.at<float>(3, 4) != 2.5f;
+        bad += m.clone().data == m.data;
+        return bad;
+    }
+    if (argc == 8 && std::string(argv[1]) == "run") {
+        const int h = std::atoi(argv[4]), w = std::atoi(argv[5]), d = std::atoi(argv[6]);
+        Mat l(h, w, CV_8UC1), r(h, w, CV_8UC1);
+        std::ifstream fl(argv[2], std::ios::binary), fr(argv[3], std::ios::binary);
+        fl.read(reinterpret_cast<char *>(l.data), (std::streamsize)h * w);
+        fr.read(reinterpret_cast<char *>(r.data), (std::streamsize)h * w);
+        if (!fl || !fr) return 2;
+        sgm_amd::SGMSolverPtr sgm = std::make_shared<sgm_amd::SGM>(h, w, 1, d);
+        sgm->process(l, r);
+        const Mat &disp = sgm->get_disp();
+        Mat view;
+        sgm->show_disp(view);
+        if (view.rows != 2 * h || view.cols != w) return 3;
+        std::ofstream fo(argv[7], std::ios::binary);
+        for (int i = 0; i < disp.rows; ++i)
+            fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
+        return fo ? 0 : 4;
+    }
+    std::fprintf(stderr, "usage: %s nodevice | run L R H W D OUT\n", argv[0]);
+    return 2;
+}

@@ -1,0 +1,71 @@
+"""Pair sharding + gather to rank 0 (stereo_matching_amd/distributed.py) with
+world_size 2 on the gloo backend (CPU).  Each rank computes its pairs with the
+oracle (test infrastructure) on tiny synthetic pairs; rank 0 checks the
+gathered batch against a single-process run."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from stereo_matching_amd import distributed, synthetic
+
+H, W, D, N = 24, 80, 32, 5
+
+
+def _pairs():
+    return [synthetic.stereo_pair(H, W, D, pair_index=i) for i in range(N)]
+
+
+def _compute(pair):
+    import oracle
+    return torch.from_numpy(oracle.process(pair[0], pair[1], D, views=1)["sub"])
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = distributed.process_batch(_pairs(), _compute)
+        q.put((rank, None if out is None else out.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_round_robin():
+    assert distributed.shard(8, 3, 8) == [3]
+    assert distributed.shard(5, 0, 2) == [0, 2, 4]
+    assert distributed.shard(5, 1, 2) == [1, 3]
+    assert sorted(i for r in range(3) for i in distributed.shard(7, r, 3)) == list(range(7))
+    with pytest.raises(ValueError):
+        distributed.shard(4, 2, 2)
+
+
+def test_gather_world2_gloo():
+    import oracle
+    oracle.build()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None
+    want = np.stack([_compute(p).numpy() for p in _pairs()])
+    assert res[0].shape == (N, H, W)
+    assert np.array_equal(res[0].view(np.uint32), want.view(np.uint32))
