@@ -70,7 +70,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
         load_v<V>(cb[u], a.cost + pc.off + e0, active);
-        if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+        if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
         pc.advance_upto(n, W, D, WD);
     }
 
@@ -99,15 +99,15 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
         const float nmin = wave_min(lm);
 
         if constexpr (MODE == SWEEP_STORE_L) {
-            store_v<V>(a.acc_out + cc.off + e0, L, active);
+            store_v_nt<V>(a.acc_out + cc.off + e0, L, active);
             if (lane == 0) a.min_out[cc.off / D] = nmin;
         } else if constexpr (MODE == SWEEP_INIT) {
-            store_v<V>(a.acc_out + cc.off + e0, L, active);
+            store_v_nt<V>(a.acc_out + cc.off + e0, L, active);
         } else {
             float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) o[v] = ai[v] + L[v];
-            store_v<V>(a.acc_out + cc.off + e0, o, active);
+            store_v_nt<V>(a.acc_out + cc.off + e0, o, active);
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) prev[v] = L[v];
@@ -117,7 +117,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
             // refill this ring slot only after its old contents are dead, so
             // the new load lands in the same registers (no copy, no wait)
             load_v<V>(cb[u], a.cost + pc.off + e0, active);
-            if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
+            if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
             pc.advance_upto(n, W, D, WD);
         }
     };
@@ -268,8 +268,8 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     float ab[K][V], sb[K][V];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
-        if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
-        if (NEED_S) load_v<V>(sb[u], a.s_in + pc.off + e0, active);
+        if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
+        if (NEED_S) load_v_nt<V>(sb[u], a.s_in + pc.off + e0, active);
         pc.advance_upto(n, W, D, WD);
     }
 
@@ -348,12 +348,12 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
                     float o[V];
 #pragma unroll
                     for (int v = 0; v < V; ++v) o[v] = lf[kk][v] + L[v];
-                    store_v<V>(a.out + bc.off + e0, o, active);
+                    store_v_nt<V>(a.out + bc.off + e0, o, active);
                 } else if constexpr (MODE == PAIR_ACC) {
                     float o[V];
 #pragma unroll
                     for (int v = 0; v < V; ++v) o[v] = (ab[r][v] + lf[kk][v]) + L[v];
-                    store_v<V>(a.out + bc.off + e0, o, active);
+                    store_v_nt<V>(a.out + bc.off + e0, o, active);
                 } else if constexpr (FINAL) {
                     float tot[V];
 #pragma unroll
@@ -365,8 +365,8 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
                 for (int v = 0; v < V; ++v) prevb[v] = L[v];
                 pminb = nmin;
                 bc.advance(W, D, WD);
-                if (NEED_ACC) load_v<V>(ab[r], a.acc_in + pc.off + e0, active);
-                if (NEED_S) load_v<V>(sb[r], a.s_in + pc.off + e0, active);
+                if (NEED_ACC) load_v_nt<V>(ab[r], a.acc_in + pc.off + e0, active);
+                if (NEED_S) load_v_nt<V>(sb[r], a.s_in + pc.off + e0, active);
                 pc.advance_upto(n, W, D, WD);
             }
         }
@@ -453,7 +453,10 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
     constexpr bool FINAL = MODE == PAIR_FINAL;
     constexpr int NW = FINAL ? 3 : 2;
-    constexpr bool NEED_ACC = MODE != PAIR_INIT2;
+    // FINAL: the backward wave streams S12 through its ring and the WTA wave
+    // adds T last (total = ((S12 + L3) + L4) + T), so each of the three waves
+    // keeps one stream in flight
+    constexpr bool NEED_ACC = MODE == PAIR_ACC;
     constexpr bool NEED_S = FINAL;
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
@@ -571,8 +574,8 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         float ab[RD][V], sb[RD][V];
 #pragma unroll
         for (int u = 0; u < RD; ++u) {
-            if (NEED_ACC) load_v<V>(ab[u], a.acc_in + pc.off + e0, active);
-            if (NEED_S) load_v<V>(sb[u], a.s_in + pc.off + e0, active);
+            if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
+            if (NEED_S) load_v_nt<V>(sb[u], a.s_in + pc.off + e0, active);
             pc.advance_upto(n, W, D, WD);
         }
         float prevb[V];
@@ -603,25 +606,25 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                         float o[V];
 #pragma unroll
                         for (int v = 0; v < V; ++v) o[v] = lf[v] + Lr[v];
-                        store_v<V>(a.out + bc.off + e0, o, active);
+                        store_v_nt<V>(a.out + bc.off + e0, o, active);
                     } else if constexpr (MODE == PAIR_ACC) {
                         float o[V];
 #pragma unroll
                         for (int v = 0; v < V; ++v) o[v] = (ab[q][v] + lf[v]) + Lr[v];
-                        store_v<V>(a.out + bc.off + e0, o, active);
+                        store_v_nt<V>(a.out + bc.off + e0, o, active);
                     } else {
-                        float tot[V];
+                        // X = (S12 + L3) + L4
+                        float x[V];
 #pragma unroll
-                        for (int v = 0; v < V; ++v) tot[v] = ((sb[q][v] + lf[v]) + Lr[v]) + ab[q][v];
-                        store_lds_v<V>(&F->t[buf][r][e0], tot);
-                        if (lane == 0) F->p[buf][r] = (long long)bc.i * W + bc.j;
+                        for (int v = 0; v < V; ++v) x[v] = (sb[q][v] + lf[v]) + Lr[v];
+                        store_lds_v<V>(&F->t[buf][r][e0], x);
                     }
 #pragma unroll
                     for (int v = 0; v < V; ++v) prevb[v] = Lr[v];
                     pminb = nmin;
                     bc.advance(W, D, WD);
-                    if (NEED_ACC) load_v<V>(ab[q], a.acc_in + pc.off + e0, active);
-                    if (NEED_S) load_v<V>(sb[q], a.s_in + pc.off + e0, active);
+                    if (NEED_ACC) load_v_nt<V>(ab[q], a.acc_in + pc.off + e0, active);
+                    if (NEED_S) load_v_nt<V>(sb[q], a.s_in + pc.off + e0, active);
                     pc.advance_upto(n, W, D, WD);
                 }
             }
@@ -645,13 +648,58 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     } else if constexpr (FINAL) {
         __builtin_amdgcn_s_setprio(1);
         // ------------------------------------------------- WTA (wave 2)
-        bar();
-        bar();
-        for (int c = 0; c < nseg; ++c) {
-            wta_consume_chunk<V, K>(F->t[c & 1], F->p[c & 1], c == nseg - 1 ? r0 : K, lane, g.D,
-                                    a.uniq, a.disp, a.sub);
+        // total = X + T (X = (S12 + L3) + L4 from the LDS ring), then WTA,
+        // uniqueness and sub-pixel over the chunk.  T rows for the next chunk
+        // are loaded while this one is processed.  Chunk c, slot r is pixel
+        // (H-1 - (cK + r), path): L4 walks the column upward.
+        constexpr int LPP = 64 / K;                  // lanes per pixel
+        constexpr int QQ = (FULL ? 64 * V : 32) / LPP;  // disparities per lane
+        static_assert(QQ % 4 == 0, "T rows load as float4");
+        const int px = lane / LPP, d0 = (lane - px * LPP) * QQ;
+        auto tload = [&](float (&t)[QQ], int c) {
+            const int cnt = c == nseg - 1 ? r0 : K;
+            const int r = px < cnt ? px : 0;
+            const long long pix = (long long)(H - 1 - (c * K + r)) * W + path;
+            const float *src = a.acc_in + pix * D + d0;
+#pragma unroll
+            for (int k = 0; k < QQ; k += 4) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t[k + e] = __builtin_nontemporal_load(src + k + e);
+            }
+        };
+        // T for chunk c+2 is issued while chunk c is consumed (3 buffers)
+        auto chunk = [&](const float (&t)[QQ], float (&tn)[QQ], int c) {
+            tload(tn, c + 2 < nseg ? c + 2 : nseg - 1);
+            const int cnt = c == nseg - 1 ? r0 : K;
+            if (px < cnt) {
+                float *row = &F->t[c & 1][px][d0];
+#pragma unroll
+                for (int k = 0; k < QQ; k += 4) {
+                    float4 x4 = *reinterpret_cast<float4 *>(row + k);
+                    x4.x = x4.x + t[k];
+                    x4.y = x4.y + t[k + 1];
+                    x4.z = x4.z + t[k + 2];
+                    x4.w = x4.w + t[k + 3];
+                    *reinterpret_cast<float4 *>(row + k) = x4;
+                }
+            }
+            wta_consume_chunk_at<V, K>(F->t[c & 1], (long long)(H - 1 - c * K) * W + path,
+                                       -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
             bar();
+        };
+        float t0[QQ], t1[QQ], t2[QQ];
+        tload(t0, 0);
+        tload(t1, nseg > 1 ? 1 : 0);
+        bar();
+        bar();
+        int c = 0;
+        for (; c + 2 < nseg; c += 3) {
+            chunk(t0, t2, c);
+            chunk(t1, t0, c + 1);
+            chunk(t2, t1, c + 2);
         }
+        if (c < nseg) chunk(t0, t2, c);
+        if (c + 1 < nseg) chunk(t1, t0, c + 1);
     }
 #ifdef SGM_STAMPS
     if (lane == 0) {

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     };
 
     if (!FILTER) {
-        for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
+        for (int j = 0; j < W; ++j) __builtin_nontemporal_store(raw(j), o + (size_t)j * D);
         return;
     }
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, U = COSTH_U;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
 #pragma unroll
-    for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
+    for (int p = 0; p < LAG; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
     const int T = W - 2 * HALF;
     // hist[0] is what step t subtracts: raw[t] for t < LAG, output t-LAG after
     float hist[LAG > 0 ? LAG : 1];
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     for (int p = 0; p < LAG; ++p) hist[p] = raw(p);
     auto step = [&](int t, float rw) {
         const float v = div_win<WIN>(sum);
-        o[(size_t)(LAG + t) * D] = v;
+        __builtin_nontemporal_store(v, o + (size_t)(LAG + t) * D);
         sum += rw;
         float a;
         if constexpr (LAG == 0) {
@@ -205,8 +205,8 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
         t += U;
     }
     for (; t < T - 1; ++t) step(t, raw(WIN + t));
-    if (T >= 1) o[(size_t)(LAG + T - 1) * D] = div_win<WIN>(sum);
-    for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
+    if (T >= 1) __builtin_nontemporal_store(div_win<WIN>(sum), o + (size_t)(LAG + T - 1) * D);
+    for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
 }
 
 // Fallback for rows too wide to stage in LDS (W*16 B > 64 KiB): census words
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
         return hamming(a, b);
     };
     if (!FILTER) {
-        for (int j = 0; j < W; ++j) o[(size_t)j * D] = raw(j);
+        for (int j = 0; j < W; ++j) __builtin_nontemporal_store(raw(j), o + (size_t)j * D);
         return;
     }
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1;
@@ -241,12 +241,12 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
 #pragma unroll
-    for (int p = 0; p < LAG; ++p) o[(size_t)p * D] = raw(p);
+    for (int p = 0; p < LAG; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
     const int T = W - 2 * HALF;
     float o1 = 0.0f, o2 = 0.0f;
     for (int t = 0; t < T; ++t) {
         const float v = div_win<WIN>(sum);
-        o[(size_t)(LAG + t) * D] = v;
+        __builtin_nontemporal_store(v, o + (size_t)(LAG + t) * D);
         if (t == T - 1) break;
         sum += raw(WIN + t);
         float a;
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
         o2 = o1;
         o1 = v;
     }
-    for (int p = LAG + T; p < W; ++p) o[(size_t)p * D] = raw(p);
+    for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
 }
 
 template <int VIEW, int WIN, bool SKY, bool FILTER>

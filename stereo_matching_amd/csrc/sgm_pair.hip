@@ -59,14 +59,14 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     const int T = H - 2 * HALF;
 
     float raw0[V], rawl[V], sum[V], o1[V];
-    load_v<V>(raw0, col, active);
-    load_v<V>(rawl, col + (size_t)(H - 1) * stride, active);  // the only row below LAG+T (WIN=3)
+    load_v_nt<V>(raw0, col, active);
+    load_v_nt<V>(rawl, col + (size_t)(H - 1) * stride, active);  // the only row below LAG+T (WIN=3)
 #pragma unroll
     for (int v = 0; v < V; ++v) sum[v] = 0.0f;
 #pragma unroll
     for (int k = 0; k < WIN; ++k) {
         float r[V];
-        load_v<V>(r, col + (size_t)k * stride, active);
+        load_v_nt<V>(r, col + (size_t)k * stride, active);
 #pragma unroll
         for (int v = 0; v < V; ++v) sum[v] += r[v];
     }
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     float ring[PF][V];
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        load_v<V>(ring[u], col + (size_t)min(LA + u, H - 1) * stride, active);
+        load_v_nt<V>(ring[u], col + (size_t)min(LA + u, H - 1) * stride, active);
 
     float prev[V];
 #pragma unroll
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
 #pragma unroll
         for (int v = 0; v < V; ++v) prev[v] = L[v];
         pmin = nmin;
-        if (refill) load_v<V>(ring[u], col + (size_t)min(i + LA + PF, H - 1) * stride, active);
+        if (refill) load_v_nt<V>(ring[u], col + (size_t)min(i + LA + PF, H - 1) * stride, active);
     };
     int i0 = 0;
     for (; i0 + PF <= H; i0 += PF) {
