@@ -159,6 +159,8 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     const long long st_t0 = __builtin_amdgcn_s_memtime();
 #endif
     constexpr int K = family_k<FD == 0 ? PAIR_H : (FD == 2 ? PAIR_V : PAIR_D2), V>();
+    static_assert(PF % K == 0, "the ring covers whole checkpoint segments");
+    constexpr bool DIAG = FD == 5;
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -168,51 +170,62 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     const int e0 = lane * V;
     const bool active = FULL || e0 < g.D;
     float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
-    int next_ck = r0 - 1, ck_i = 0;
 
+    // The chain is walked from a virtual start vs = K - r0 steps before
+    // position 0 so that checkpoint m (the state after position r0-1 + mK)
+    // falls on the last step of every K-step block: the stores sit at fixed
+    // places in the unrolled loop, with no branch.  Virtual positions read
+    // zero costs from a.zero; with the state starting at L = 0, minL = 0 a
+    // step on a zero cost keeps it at 0 (P1, P2 >= 0), and the first real step
+    // then yields L = C, the reference's path start (SGM.cpp:93-98).  Block
+    // nseg-1 stores into the unused last slot.
+    const int vs = K - r0;
     Cursor<FD> cc, pc;
     cc.init(path, H, W, g.D);
     pc.init(path, H, W, g.D);
+    int ppos = -vs;  // position of the next ring refill
+    auto fetch = [&](float (&dst)[V]) {
+        const float *src = ppos >= 0 ? a.cost + pc.off : a.zero;
+        load_v<V>(dst, src + e0, active);
+        pc.advance_if(ppos >= 0 && pc.k < n - 1, W, D, WD);
+        ++ppos;
+    };
     float cb[PF][V];
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-        load_v<V>(cb[u], a.cost + pc.off + e0, active);
-        pc.advance_upto(n, W, D, WD);
-    }
+    for (int u = 0; u < PF; ++u) fetch(cb[u]);
     float prev[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+    for (int v = 0; v < V; ++v) prev[v] = 0.0f;
     float pmin = 0.0f;
+    int cpos = -vs;  // position of the next step
 
     auto step = [&](int u, bool refill) {
         float L[V];
         dp_step<V>(prev, pmin, cb[u], L, a.p1, a.p2);
-        const bool st = cc.start(W);
+        if constexpr (DIAG) {
+            // a wrapped diagonal restarts where it meets the image edge
+            const bool st = cpos > 0 && cc.start(W);
 #pragma unroll
-        for (int v = 0; v < V; ++v) L[v] = st ? cb[u][v] : L[v];
-        const float nmin = wave_min(lane_min(L));
-        if (cc.k == next_ck && ck_i < nseg - 1) {
-            store_v<V>(ck + (size_t)ck_i * g.D, L, active);
-            ++ck_i;
-            next_ck += K;
+            for (int v = 0; v < V; ++v) L[v] = st ? cb[u][v] : L[v];
         }
+        const float nmin = wave_min(lane_min(L));
+        if (u % K == K - 1) store_v<V>(ck + (size_t)((cpos - r0 + 1) / K) * g.D, L, active);
 #pragma unroll
         for (int v = 0; v < V; ++v) prev[v] = L[v];
         pmin = nmin;
-        cc.advance(W, D, WD);
-        if (refill) {
-            load_v<V>(cb[u], a.cost + pc.off + e0, active);
-            pc.advance_upto(n, W, D, WD);
-        }
+        if constexpr (DIAG) cc.advance_if(cpos >= 0, W, D, WD);
+        ++cpos;
+        if (refill) fetch(cb[u]);
     };
+    const int total = nseg * K;
     int k0 = 0;
-    for (; k0 + PF <= n; k0 += PF) {
+    for (; k0 + PF <= total; k0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) step(u, true);
     }
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        if (k0 + u < n) step(u, false);
+        if (k0 + u < total) step(u, false);
 #ifdef SGM_STAMPS
     stamp_flush(FD == 0 ? 5 : (FD == 5 ? 6 : 7), st_t0);
 #endif

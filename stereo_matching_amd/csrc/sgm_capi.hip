@@ -46,6 +46,7 @@ struct sgm_handle {
     float *d_sub[2];      // sub-pixel disparity
     float *d_out;         // LR-checked output (host API)
     float *d_min;         // minL (stage_path)
+    float *d_zero;        // 256 zero floats (PairArgs::zero)
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
     uint8_t *h_pin;       // pinned host staging for sgm_process (allocated on first use)
     size_t h_pin_bytes;
@@ -106,6 +107,8 @@ bool valid_params(const sgm_params *p, char *why, size_t n) {
     const int H = p->height / p->scale, W = p->width / p->scale;
     if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
     if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
+    // the path DP's start handling relies on non-negative penalties (SGM.cpp:27-28 uses 10, 100)
+    if (p->p1 < 0 || p->p2 < 0) { snprintf(why, n, "p1 and p2 must be >= 0"); return false; }
     if ((size_t)H * W > (size_t)0x7fffffff) { snprintf(why, n, "image too large"); return false; }
     return true;
 }
@@ -127,6 +130,7 @@ void free_all(sgm_handle *h) {
     }
     (void)hipFree(h->d_out);
     (void)hipFree(h->d_min);
+    (void)hipFree(h->d_zero);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
     h->h_pin = nullptr;
     for (auto &v : h->d_ck)
@@ -196,6 +200,7 @@ SweepArgs sweep_args(const sgm_handle *h) {
 
 sgm::PairArgs pair_args(const sgm_handle *h) {
     sgm::PairArgs a{};
+    a.zero = h->d_zero;
     a.p1 = (float)h->p.p1;
     a.p2 = (float)h->p.p2;
     a.uniq = h->p.uniqueness;
@@ -431,6 +436,9 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         }
         if (!rc) rc = dalloc(h, &h->d_out, npx);
         if (!rc) rc = dalloc(h, &h->d_min, npx);
+        if (!rc) rc = dalloc(h, &h->d_zero, 256);
+        if (!rc && hipMemset(h->d_zero, 0, 256 * sizeof(float)) != hipSuccess)
+            rc = set_err(h, SGM_ERR_HIP, "hipMemset of the zero page failed");
     } while (0);
     if (rc) {
         fprintf(stderr, "sgm_create: %s\n", h->err[0] ? h->err : "HIP stream/event creation failed");

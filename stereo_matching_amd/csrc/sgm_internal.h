@@ -56,6 +56,8 @@ struct PairArgs {
     float *ckpt;
     uint16_t *disp;
     float *sub;
+    const float *zero;   // >= 256 zero floats: the cost of the virtual positions
+                         // that align forward passes with their checkpoints
     float p1, p2, uniq;
 };
 

@@ -10,43 +10,12 @@
 using namespace sgm;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float red_bcast(float x) {
-    x = fminf(x, movdppf<DPP_QP_1032>(x));
-    x = fminf(x, movdppf<DPP_QP_2301>(x));
-    x = fminf(x, movdppf<DPP_HALF_MIRROR>(x));
-    x = fminf(x, movdppf<DPP_MIRROR>(x));
-    // rows 1,3 take min with row 0,2's last lane; rows 2,3 with lane 31
-    asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-                 "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
-                 : "+v"(x));
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
-}
-
-// neighbour minimum with the edge lane keeping its own value: min(src[l-1], a)
-// (SHR) or min(a, src[l+1]) (SHL); bound_ctrl off, old = a
-template <int CTRL>
-__device__ __forceinline__ float nbmin(float src, float a) {
-    float d = a;
-    if constexpr (CTRL == DPP_WAVE_SHR1)
-        asm("s_nop 1\n\tv_min_f32_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf"
-                     : "+v"(d) : "v"(src));
-    else
-        asm("s_nop 1\n\tv_min_f32_dpp %0, %1, %0 wave_shl:1 row_mask:0xf bank_mask:0xf"
-                     : "+v"(d) : "v"(src));
-    return d;
-}
-
 __device__ __forceinline__ void dp_lean2(f2 &prev, float &pmin, f2 c, float p1, float p2) {
-    const float n0 = nbmin<DPP_WAVE_SHR1>(prev.y, prev.y);  // min(L[d-1], L[d+1]) for d = 2l
-    const float n1 = nbmin<DPP_WAVE_SHL1>(prev.x, prev.x);  // for d = 2l+1
-    f2 t = f2{n0, n1} + p1;
-    const float pp2 = pmin + p2;
-    f2 m;
-    m.x = fminf(fminf(prev.x, t.x), pp2);
-    m.y = fminf(fminf(prev.y, t.y), pp2);
-    const f2 L = m + (c - pmin);
-    pmin = red_bcast(fminf(L.x, L.y));
-    prev = L;
+    const float pv[2] = {prev.x, prev.y}, cv[2] = {c.x, c.y};
+    float L[2];
+    dp_step<2>(pv, pmin, cv, L, p1, p2);
+    pmin = wave_min(fminf(L[0], L[1]));
+    prev = f2{L[0], L[1]};
 }
 
 template <int LEAN>
@@ -82,6 +51,46 @@ __global__ __launch_bounds__(64) void chain(const float *__restrict__ cin, float
     out[(bid_x() * 64 + lane) * 3 + 1] = L[1];
     out[(bid_x() * 64 + lane) * 3 + 2] = pmin;
     if (lane == 0) cyc[bid_x()] = t1 - t0;
+}
+
+// NCH independent chains interleaved in one wave
+template <int NCH>
+__global__ __launch_bounds__(64) void chain_multi(const float *__restrict__ cin, float *out, long long *cyc,
+                                                  int nsteps) {
+    const int lane = tid_x();
+    float c[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) c[k][v] = cin[((bid_x() & 7) * 4 * 64 + k * 64 + lane) * 2 + v];
+    f2 Lp[NCH];
+    float pmin[NCH];
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) { Lp[q] = f2{c[q & 3][0] + q, c[q & 3][1]}; pmin[q] = 0.0f; }
+    const long long t0 = clock64();
+    for (int s = 0; s < nsteps; s += 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int q = 0; q < NCH; ++q) dp_lean2(Lp[q], pmin[q], f2{c[k][0], c[k][1]}, 3.0f, 20.0f);
+    }
+    const long long t1 = clock64();
+    float acc = 0;
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) acc += Lp[q].x + Lp[q].y + pmin[q];
+    out[bid_x() * 64 + lane] = acc;
+    if (lane == 0) cyc[bid_x()] = t1 - t0;
+}
+
+template <int NCH>
+static void run_multi(int nblocks, const float *dc, float *dout, long long *dcyc) {
+    const int nsteps = 4096;
+    chain_multi<NCH><<<nblocks, 64>>>(dc, dout, dcyc, nsteps);
+    (void)hipDeviceSynchronize();
+    long long cyc = 0;
+    (void)hipMemcpy(&cyc, dcyc, sizeof(cyc), hipMemcpyDeviceToHost);
+    printf("chains/wave %d blocks %5d: %6.1f clk per step of all chains, %6.1f per chain-step\n", NCH,
+           nblocks, (double)cyc / nsteps, (double)cyc / nsteps / NCH);
 }
 
 template <int LEAN>
@@ -131,6 +140,12 @@ int main() {
         const double t1 = run<1>(nb, 4096, dc, dout, dcyc, &c1);
         printf("blocks %5d: current %6.1f clk/step %7.2f ns/step | lean %6.1f clk/step %7.2f ns/step\n",
                nb, c0, t0, c1, t1);
+    }
+    for (int nb : {1, 375}) {
+        run_multi<1>(nb, dc, dout, dcyc);
+        run_multi<2>(nb, dc, dout, dcyc);
+        run_multi<3>(nb, dc, dout, dcyc);
+        run_multi<4>(nb, dc, dout, dcyc);
     }
     return 0;
 }
