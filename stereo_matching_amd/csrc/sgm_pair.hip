@@ -77,9 +77,11 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     for (int u = 0; u < PF; ++u)
         load_v_nt<V>(ring[u], col + (size_t)min(LA + u, H - 1) * stride, active);
 
+    // L = 0, minL = 0 before row 0 makes the first step yield L = C (the
+    // path start, SGM.cpp:161-170) without a per-row select (P1, P2 >= 0)
     float prev[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+    for (int v = 0; v < V; ++v) prev[v] = 0.0f;
     float pmin = 0.0f;
 
     auto row = [&](int i, int u, bool refill) {
@@ -108,8 +110,6 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
         // L3 forward step on the freshly filtered row
         float L[V];
         dp_step<V>(prev, pmin, c, L, a.p1, a.p2);
-#pragma unroll
-        for (int v = 0; v < V; ++v) L[v] = i == 0 ? c[v] : L[v];
         const float nmin = wave_min(lane_min(L));
         if (i == next_ck && ck_i < nseg - 1) {
             store_v<V>(ck + (size_t)ck_i * g.D, L, active);
