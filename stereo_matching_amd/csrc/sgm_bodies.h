@@ -184,15 +184,33 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     cc.init(path, H, W, g.D);
     pc.init(path, H, W, g.D);
     int ppos = -vs;  // position of the next ring refill
+    // rows (FD 0): a plain running pointer; positions past the row's end read
+    // the next row or the volume guard (kVolGuard) and are never consumed
+    const float *hrow = a.cost + (size_t)path * W * g.D;
     auto fetch = [&](float (&dst)[V]) {
-        const float *src = ppos >= 0 ? a.cost + pc.off : a.zero;
-        load_v<V>(dst, src + e0, active);
-        pc.advance_if(ppos >= 0 && pc.k < n - 1, W, D, WD);
+        if constexpr (FD == 0) {
+            const float *src = ppos >= 0 ? hrow + (size_t)ppos * g.D : a.zero;
+            load_v<V>(dst, src + e0, active);
+        } else {
+            const float *src = ppos >= 0 ? a.cost + pc.off : a.zero;
+            load_v<V>(dst, src + e0, active);
+            pc.advance_if(ppos >= 0 && pc.k < n - 1, W, D, WD);
+        }
         ++ppos;
     };
     float cb[PF][V];
 #pragma unroll
     for (int u = 0; u < PF; ++u) fetch(cb[u]);
+    // in the main loop every refill position is >= PF - vs > 0
+    const float *hnext = hrow + (size_t)ppos * g.D + e0;
+    auto refetch = [&](float (&dst)[V]) {
+        if constexpr (FD == 0) {
+            load_v<V>(dst, hnext, active);
+            hnext += g.D;
+        } else {
+            fetch(dst);
+        }
+    };
     float prev[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) prev[v] = 0.0f;
@@ -215,7 +233,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
         pmin = nmin;
         if constexpr (DIAG) cc.advance_if(cpos >= 0, W, D, WD);
         ++cpos;
-        if (refill) fetch(cb[u]);
+        if (refill) refetch(cb[u]);
     };
     const int total = nseg * K;
     int k0 = 0;

@@ -424,7 +424,9 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         }
         for (int v = 0; v < h->nviews && !rc; ++v) {
             if ((rc = dalloc(h, &h->d_ch[v], nvol))) break;
-            if ((rc = dalloc(h, &h->d_c[v], nvol))) break;
+            // + guard: the row-walking forward pass prefetches up to PF
+            // positions past the end of the last row (never consumed)
+            if ((rc = dalloc(h, &h->d_c[v], nvol + sgm::kVolGuard))) break;
             if ((rc = dalloc(h, &h->d_s[v], nvol))) break;
             if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
             if ((rc = dalloc(h, &h->d_sub[v], npx))) break;

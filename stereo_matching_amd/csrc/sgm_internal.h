@@ -8,6 +8,10 @@
 
 namespace sgm {
 
+// Floats of slack after the final cost volume: row-walking prefetch rings may
+// read up to 64 positions (x D <= 256) past the last row's end.
+constexpr size_t kVolGuard = 64 * 256 + 256;
+
 // Geometry of one frame on the working (decimated) grid.
 struct Geom {
     int H, W, D;   // rows, cols, disparities
