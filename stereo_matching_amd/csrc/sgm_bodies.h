@@ -499,6 +499,13 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     const bool active = FULL || e0 < g.D;
     using full_t = std::integral_constant<bool, true>;
     using part_t = std::integral_constant<bool, false>;
+    // Rows and columns (LIN) are addressed by a base and a stride; a path
+    // starts only at position 0, handled by a zero initial state (L = 0,
+    // minL = 0 makes the first step yield L = C, P1, P2 >= 0).  Wrapped
+    // diagonals keep the cursor and the per-step restart select.
+    constexpr bool LIN = FAM != PAIR_D2;
+    const long long lin_base = FAM == PAIR_H ? (long long)path * WD : (long long)path * D;
+    const long long lin_st = FAM == PAIR_H ? D : WD;
 
     if (wave == 0) {
         // H rows: the recompute chain is the slower one; V: the backward one
@@ -515,12 +522,23 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             s = s < 0 ? 0 : s;
             const int cnt = s == 0 ? r0 : K;
             const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
-            Cursor<FD> fc;
-            fc.init_at(path, pos0, H, W, g.D);
+            if constexpr (LIN) {
+                // slot kk holds position pos0 + max(kk - (K - cnt), 0)
+                const float *p0 = a.cost + lin_base + (long long)pos0 * lin_st + e0;
+                const int sh = K - cnt;
 #pragma unroll
-            for (int kk = 0; kk < K; ++kk) {
-                load_v<V>(cs[kk], a.cost + fc.off + e0, active);
-                fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
+                for (int kk = 0; kk < K; ++kk) {
+                    const int rel = kk - sh > 0 ? kk - sh : 0;
+                    load_v<V>(cs[kk], p0 + (long long)rel * lin_st, active);
+                }
+            } else {
+                Cursor<FD> fc;
+                fc.init_at(path, pos0, H, W, g.D);
+#pragma unroll
+                for (int kk = 0; kk < K; ++kk) {
+                    load_v<V>(cs[kk], a.cost + fc.off + e0, active);
+                    fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
+                }
             }
             load_v<V>(cs[K], ck + (size_t)(s > 0 ? s - 1 : 0) * g.D, active);
         };
@@ -538,24 +556,26 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                 pminf = wave_min(lane_min(pf));
             } else {  // segment 0 starts the chain
 #pragma unroll
-                for (int v = 0; v < V; ++v) pf[v] = SGM_INF;
+                for (int v = 0; v < V; ++v) pf[v] = LIN ? 0.0f : SGM_INF;
             }
             Cursor<FD> fc;
-            fc.init_at(path, pos0, H, W, g.D);
+            if constexpr (!LIN) fc.init_at(path, pos0, H, W, g.D);
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) {
                 if (FULLSEG || kk >= skip) {
                     float Lr[V];
                     dp_step<V>(pf, pminf, cs[kk], Lr, a.p1, a.p2);
-                    const bool st = fc.start(W);
+                    if constexpr (!LIN) {
+                        const bool st = fc.start(W);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) Lr[v] = st ? cs[kk][v] : Lr[v];
+                        for (int v = 0; v < V; ++v) Lr[v] = st ? cs[kk][v] : Lr[v];
+                    }
                     pminf = wave_min(lane_min(Lr));
                     store_lds_v<V>(&L.c[buf][kk][e0], cs[kk]);
                     store_lds_v<V>(&L.l[buf][kk][e0], Lr);
 #pragma unroll
                     for (int v = 0; v < V; ++v) pf[v] = Lr[v];
-                    fc.advance(W, D, WD);
+                    if constexpr (!LIN) fc.advance(W, D, WD);
                 }
             }
             bar();
@@ -602,16 +622,29 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         Cursor<BD> bc, pc;
         bc.init(bpath, H, W, g.D);
         pc.init(bpath, H, W, g.D);
+        // LIN: running offsets of the step (bo) and of the ring refill (po,
+        // position pp, held at position 0 past the chain's end)
+        long long bo = lin_base + (long long)(n - 1) * lin_st, po = bo;
+        int pp = n - 1;
+        auto padv = [&] {
+            if constexpr (LIN) {
+                po -= pp > 0 ? lin_st : 0;
+                pp = pp > 0 ? pp - 1 : 0;
+            } else {
+                pc.advance_upto(n, W, D, WD);
+            }
+        };
+        auto poff = [&] { return LIN ? po : pc.off; };
         float ab[RD][V], sb[RD][V];
 #pragma unroll
         for (int u = 0; u < RD; ++u) {
-            if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
-            if (NEED_S) load_v_nt<V>(sb[u], a.s_in + pc.off + e0, active);
-            pc.advance_upto(n, W, D, WD);
+            if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + poff() + e0, active);
+            if (NEED_S) load_v_nt<V>(sb[u], a.s_in + poff() + e0, active);
+            padv();
         }
         float prevb[V];
 #pragma unroll
-        for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
+        for (int v = 0; v < V; ++v) prevb[v] = LIN ? 0.0f : SGM_INF;
         float pminb = 0.0f;
         auto consume = [&](int c, auto full_tag, auto half_tag) {
             constexpr bool FULLSEG = decltype(full_tag)::value;
@@ -629,20 +662,23 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     load_lds_v<V>(lf, &L.l[buf][kk][e0]);
                     float Lr[V];
                     dp_step<V>(prevb, pminb, cs, Lr, a.p1, a.p2);
-                    const bool st = bc.start(W);
+                    if constexpr (!LIN) {
+                        const bool st = bc.start(W);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) Lr[v] = st ? cs[v] : Lr[v];
+                        for (int v = 0; v < V; ++v) Lr[v] = st ? cs[v] : Lr[v];
+                    }
                     const float nmin = wave_min(lane_min(Lr));
+                    const long long boff = LIN ? bo : bc.off;
                     if constexpr (MODE == PAIR_INIT2) {
                         float o[V];
 #pragma unroll
                         for (int v = 0; v < V; ++v) o[v] = lf[v] + Lr[v];
-                        store_v_nt<V>(a.out + bc.off + e0, o, active);
+                        store_v_nt<V>(a.out + boff + e0, o, active);
                     } else if constexpr (MODE == PAIR_ACC) {
                         float o[V];
 #pragma unroll
                         for (int v = 0; v < V; ++v) o[v] = (ab[q][v] + lf[v]) + Lr[v];
-                        store_v_nt<V>(a.out + bc.off + e0, o, active);
+                        store_v_nt<V>(a.out + boff + e0, o, active);
                     } else {
                         // X = (S12 + L3) + L4
                         float x[V];
@@ -653,10 +689,11 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
 #pragma unroll
                     for (int v = 0; v < V; ++v) prevb[v] = Lr[v];
                     pminb = nmin;
-                    bc.advance(W, D, WD);
-                    if (NEED_ACC) load_v_nt<V>(ab[q], a.acc_in + pc.off + e0, active);
-                    if (NEED_S) load_v_nt<V>(sb[q], a.s_in + pc.off + e0, active);
-                    pc.advance_upto(n, W, D, WD);
+                    if constexpr (LIN) bo -= lin_st;
+                    else bc.advance(W, D, WD);
+                    if (NEED_ACC) load_v_nt<V>(ab[q], a.acc_in + poff() + e0, active);
+                    if (NEED_S) load_v_nt<V>(sb[q], a.s_in + poff() + e0, active);
+                    padv();
                 }
             }
             bar();
