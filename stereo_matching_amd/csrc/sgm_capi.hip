@@ -32,6 +32,7 @@ struct sgm_handle {
     int device;
     int nviews;
     int serialize;        // SGM_SERIALIZE=1: every kernel on one stream (isolated timings)
+    int concurrent_views; // SGM_CONCURRENT_VIEWS=1: right view on a second stream
     size_t bytes;
     hipStream_t st;       // the handle's own stream (host API, stages)
     hipStream_t aux[1];      // right view (two-view frames)
@@ -288,7 +289,12 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
     const Geom g = h->g;
     int rc;
-    hipStream_t aux1 = h->serialize ? st : h->aux[0];  // right view
+    // Views run back to back on one stream by default: each view's cost
+    // volume (238.5 MB at K128) then stays resident in the 256 MB Infinity
+    // Cache through its six readers, which concurrent views would thrash
+    // (1.589 vs 1.627 ms per K128 pair).  SGM_CONCURRENT_VIEWS=1 restores the
+    // second stream.
+    hipStream_t aux1 = h->concurrent_views ? h->aux[0] : st;  // right view
     const double npx = (double)g.H * g.W;
     HIPCHK(h, timed(h, "census", npx, st, [&] {
                return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st);
@@ -401,6 +407,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
     {
         const char *ser = getenv("SGM_SERIALIZE");
         h->serialize = ser && ser[0] == '1';
+        const char *cv = getenv("SGM_CONCURRENT_VIEWS");
+        h->concurrent_views = cv && cv[0] == '1' && !h->serialize;
     }
 
     const size_t npx = (size_t)h->g.H * h->g.W;
