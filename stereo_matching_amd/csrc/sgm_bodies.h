@@ -460,7 +460,7 @@ struct SplitFinalLds {
 // NB: register buffers of segment costs in the producer (NB-1 segments of
 // loads in flight while one is recomputed); RH: the consumer's ring of
 // accumulator loads is RH*K steps deep (chunks processed RH at a time).
-template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1>
+template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1, int NWTA = 1>
 __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g, int path,
                                                 int wave, SplitLds<K, V> &L,
                                                 SplitFinalLds<K, V> *F) {
@@ -483,7 +483,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
     constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
     constexpr bool FINAL = MODE == PAIR_FINAL;
-    constexpr int NW = FINAL ? 3 : 2;
+    constexpr int NSTAGE = FINAL ? 3 : 2;  // pipeline stages (WTA waves share stage 3)
     // FINAL: the backward wave streams S12 through its ring and the WTA wave
     // adds T last (total = ((S12 + L3) + L4) + T), so each of the three waves
     // keeps one stream in flight
@@ -612,7 +612,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         else if (b0 == 1) produce(cb[1], 0, part_t{});
         else produce(cb[NB - 1], 0, part_t{});
 #pragma unroll
-        for (int t = 0; t < NW - 1; ++t) bar();
+        for (int t = 0; t < NSTAGE - 1; ++t) bar();
     } else if (wave == 1) {
         // the backward chain is the critical path of the pair: issue priority
         __builtin_amdgcn_s_setprio(3);
@@ -714,19 +714,23 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         }
         if (FINAL) bar();
     } else if constexpr (FINAL) {
-        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(3);  // the WTA wave is the slowest stage of the final pipeline
         // ------------------------------------------------- WTA (wave 2)
         // total = X + T (X = (S12 + L3) + L4 from the LDS ring), then WTA,
         // uniqueness and sub-pixel over the chunk.  T rows for the next chunk
         // are loaded while this one is processed.  Chunk c, slot r is pixel
         // (H-1 - (cK + r), path): L4 walks the column upward.
-        constexpr int LPP = 64 / K;                  // lanes per pixel
+        // NWTA waves split each chunk's K pixels (KP each)
+        constexpr int KP = K / NWTA;
+        constexpr int LPP = 64 / KP;                 // lanes per pixel
         constexpr int QQ = (FULL ? 64 * V : 32) / LPP;  // disparities per lane
         static_assert(QQ % 4 == 0, "T rows load as float4");
+        const int half = wave - 2;
         const int px = lane / LPP, d0 = (lane - px * LPP) * QQ;
+        const int slot = half * KP + px;
         auto tload = [&](float (&t)[QQ], int c) {
             const int cnt = c == nseg - 1 ? r0 : K;
-            const int r = px < cnt ? px : 0;
+            const int r = slot < cnt ? slot : 0;
             const long long pix = (long long)(H - 1 - (c * K + r)) * W + path;
             const float *src = a.acc_in + pix * D + d0;
 #pragma unroll
@@ -738,9 +742,10 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         // T for chunk c+2 is issued while chunk c is consumed (3 buffers)
         auto chunk = [&](const float (&t)[QQ], float (&tn)[QQ], int c) {
             tload(tn, c + 2 < nseg ? c + 2 : nseg - 1);
-            const int cnt = c == nseg - 1 ? r0 : K;
+            const int cnt_all = c == nseg - 1 ? r0 : K;
+            const int cnt = cnt_all - half * KP < 0 ? 0 : (cnt_all - half * KP > KP ? KP : cnt_all - half * KP);
             if (px < cnt) {
-                float *row = &F->t[c & 1][px][d0];
+                float *row = &F->t[c & 1][slot][d0];
 #pragma unroll
                 for (int k = 0; k < QQ; k += 4) {
                     float4 x4 = *reinterpret_cast<float4 *>(row + k);
@@ -751,8 +756,9 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     *reinterpret_cast<float4 *>(row + k) = x4;
                 }
             }
-            wta_consume_chunk_at<V, K>(F->t[c & 1], (long long)(H - 1 - c * K) * W + path,
-                                       -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
+            wta_consume_chunk_at<V, KP>(F->t[c & 1] + half * KP,
+                                        (long long)(H - 1 - c * K - half * KP) * W + path,
+                                        -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
             bar();
         };
         float t0[QQ], t1[QQ], t2[QQ];

@@ -145,12 +145,16 @@ __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
 // S12 and T, then WTA.  Three waves (pair_split_body): wave 0 recomputes L3
 // segments from their checkpoints, wave 1 runs L4 and sums the totals into an
 // LDS ring, wave 2 runs the batched WTA on the chunk before.
+// D = 64 / 128 run two WTA waves per column (four pixels each per chunk).
 template <int V, bool FULL>
-__global__ __launch_bounds__(192) void pair_final_kernel(PairArgs a, Geom g) {
+constexpr int final_nwta() { return FULL && V <= 2 ? 2 : 1; }
+
+template <int V, bool FULL>
+__global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
     __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
-    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2>(a, g, bid_x(), wave_id(), lds.s,
-                                                    &lds);
+    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>()>(
+        a, g, bid_x(), wave_id(), lds.s, &lds);
 }
 
 // Multi-role stage kernels of the frame schedule: block ranges run different
@@ -260,10 +264,10 @@ static void launch_bwd_t(const PairArgs &a, Geom g, hipStream_t st) {
 
 static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(g.W);
-    if (g.D == 32) pair_final_kernel<1, false><<<grid, 192, 0, st>>>(a, g);
-    else if (g.D == 64) pair_final_kernel<1, true><<<grid, 192, 0, st>>>(a, g);
-    else if (g.D == 128) pair_final_kernel<2, true><<<grid, 192, 0, st>>>(a, g);
-    else pair_final_kernel<4, true><<<grid, 192, 0, st>>>(a, g);
+    if (g.D == 32) pair_final_kernel<1, false><<<grid, 64 * (2 + final_nwta<1, false>()), 0, st>>>(a, g);
+    else if (g.D == 64) pair_final_kernel<1, true><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a, g);
+    else if (g.D == 128) pair_final_kernel<2, true><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a, g);
+    else pair_final_kernel<4, true><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a, g);
 }
 
 hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipStream_t st) {
