@@ -112,7 +112,11 @@ constexpr int COSTH_U = 8;
 
 __host__ __device__ constexpr int costh_pad(int D, int scale) { return D / scale + 2 * COSTH_U; }
 
-template <int VIEW, int WIN, bool SKY, bool FILTER>
+// UNI (D >= 64, one row per wave): the census word every lane of a row needs
+// at step j -- cl[j] for the left view, cr[j] for the right -- is a uniform
+// scalar load from global memory; only the per-lane shifted row is staged in
+// LDS, which halves the staging and keeps 4K rows (3840 px) inside 64 KiB.
+template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI>
 __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
                                                      const uint64_t *__restrict__ ctr,
                                                      const uint8_t *__restrict__ sky,
@@ -120,32 +124,37 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
                                                      int R, float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int P = costh_pad(D, scale), RS = W + 2 * P;
+    constexpr int NS = UNI ? 1 : 2;  // staged census rows per image row
     uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
-    uint64_t *sr = sl + (size_t)R * RS;
-    uint8_t *ss = reinterpret_cast<uint8_t *>(sr + (size_t)R * RS);
+    uint64_t *sr = sl + (UNI ? 0 : (size_t)R * RS);
+    uint8_t *ss = reinterpret_cast<uint8_t *>(sl + (size_t)NS * R * RS);
     const int row0 = bid_x() * R;
     for (int idx = tid_x(); idx < R * RS; idx += R * D) {
         const int r = idx / RS, jp = idx - r * RS, i = row0 + r;
         const int j = clampi(jp - P, 0, W - 1);
         if (i < H) {
-            sl[idx] = ctl[(size_t)i * W + j];
-            sr[idx] = ctr[(size_t)i * W + j];
+            if (!UNI || VIEW == 1) sl[idx] = ctl[(size_t)i * W + j];
+            if (!UNI || VIEW == 0) sr[idx] = ctr[(size_t)i * W + j];
             if (SKY) ss[idx] = sky[(size_t)i * sky_pitch + j];
         }
     }
     __syncthreads();
-    const int r = tid_x() / D, d = tid_x() - r * D;
+    const int r = UNI ? uniform(tid_x() / D) : tid_x() / D, d = tid_x() - r * D;
     const int i = row0 + r;
     if (i >= H) return;
     const int ds = d / scale;
     // raw(j) reads cl[j (+ds)] and cr[j (-ds)] through the padded rows
     const uint64_t *cl = sl + (size_t)r * RS + P + (VIEW == 1 ? ds : 0);
     const uint64_t *cr = sr + (size_t)r * RS + P - (VIEW == 0 ? ds : 0);
+    const uint64_t *cu = (VIEW == 0 ? ctl : ctr) + (size_t)i * W;  // UNI: the uniform row
     const uint8_t *sk = ss + (size_t)r * RS + P;
     float *o = out + (size_t)i * W * D + d;
 
+    auto word_l = [&](int j) { return UNI && VIEW == 0 ? cu[j < W - 1 ? j : W - 1] : cl[j]; };
+    auto word_r = [&](int j) { return UNI && VIEW == 1 ? cu[j < W - 1 ? j : W - 1] : cr[j]; };
+
     auto raw = [&](int j) -> float {
-        const float c = hamming(cl[j], cr[j]);
+        const float c = hamming(word_l(j), word_r(j));
         if (SKY) {
             const float sv = d == 0 ? 0.0f : 999999.0f;
             return sk[j] == 255 ? sv : c;
@@ -263,14 +272,22 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
 template <int VIEW, int WIN, bool SKY, bool FILTER>
 static void launch_cost_h_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                             int sky_pitch, Geom g, float *out, hipStream_t st) {
-    const size_t row_bytes =
-        (size_t)(g.W + 2 * costh_pad(g.D, g.scale)) * (16 + (SKY ? 1 : 0));
+    // stage both census rows when they fit (faster: LDS reads for both
+    // operands); rows too wide for that (4K) stage one and load the uniform
+    // operand as scalars
+    const size_t rs = (size_t)(g.W + 2 * costh_pad(g.D, g.scale));
+    const bool uni = g.D >= 64 && rs * (16 + (SKY ? 1 : 0)) > (size_t)COSTH_MAX_LDS;
+    const size_t row_bytes = rs * ((uni ? 8 : 16) + (SKY ? 1 : 0));
     int R = (int)(COSTH_MAX_LDS / row_bytes);
     if (R > 256 / g.D) R = 256 / g.D;
     if (R >= 1) {
         const size_t smem = (size_t)R * row_bytes;
-        cost_h_kernel<VIEW, WIN, SKY, FILTER><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
-            ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
+        if (uni)
+            cost_h_kernel<VIEW, WIN, SKY, FILTER, true><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+                ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
+        else
+            cost_h_kernel<VIEW, WIN, SKY, FILTER, false><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+                ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
     } else {
         const int rpb = 256 / g.D;
         cost_h_global_kernel<VIEW, WIN, SKY, FILTER><<<dim3((g.H + rpb - 1) / rpb), 256, 0, st>>>(
