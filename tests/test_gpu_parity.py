@@ -25,6 +25,11 @@ CASES = [
     (42, 150, 128, 2, "noise", True, True),
     (20, 70, 64, 1, "road", False, False),   # border-heavy: W just above D
     (3, 5, 32, 1, "noise", False, True),     # smallest legal frame (5x3 window)
+    (200, 60, 32, 1, "road", False, True),   # tall: diagonal chains wrap 3+ times (H > W)
+    (24, 130, 128, 1, "noise", False, True), # W just above D = 128
+    (37, 257, 64, 1, "road", True, True),    # odd sizes with a sky mask
+    (9, 300, 256, 1, "noise", False, True),  # few rows: one partial vertical segment
+    (130, 66, 64, 2, "noise", True, True),   # tall, decimated, sky
 ]
 IDS = [f"{h}x{w}_D{D}_s{s}_{k}{'_sky' if sk else ''}{'' if b else '_noblur'}"
        for h, w, D, s, k, sk, b in CASES]
