@@ -70,11 +70,18 @@ def bytes_per_elem(name: str, D: int) -> float:
     return 0.0
 
 
-BYTES_PER_PIXEL = {"census": 9, "lr": 12}
+BYTES_PER_PIXEL = {"census": 9, "lr": 12,
+                   # post_filter (sgm_post.hip), per pixel and launch: the fill reads
+                   # the original and working maps (8); labelling reads the map and
+                   # writes label + count (12); the area test reads map, 2 labels,
+                   # area and writes the map (16); count/merge touch few pixels
+                   "post_median": 8, "post_cc_local": 12, "post_cc_apply": 16,
+                   "post_cc_count": 4, "post_cc_merge": 0}
 
 
 def algorithmic_bytes(name: str, elems: float, D: int) -> float:
     if name in BYTES_PER_PIXEL:
+        # per-pixel classes report elems = pixels (census: W*H; post_*: W*H)
         return BYTES_PER_PIXEL[name] * elems
     return bytes_per_elem(name, D) * elems
 
@@ -89,6 +96,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=3,
                     help="frames of the CPU baseline sample (median reported)")
     ap.add_argument("--no-profile-pass", action="store_true")
+    ap.add_argument("--post-filter", action="store_true",
+                    help="end each step with post_filter() on the GPU (SGM.cpp:821; V=2 configs)")
     ap.add_argument("--host-io", action="store_true",
                     help="also time sgm_process on host buffers (PCIe-inclusive, not `value`)")
     return ap.parse_args()
@@ -121,7 +130,7 @@ def main():
     d_out = torch.empty((h, w), dtype=torch.float32, device=dev)
     gather = [torch.empty_like(d_out) for _ in range(world)] if (world > 1 and rank == 0) else None
 
-    sgm = SGM(h, w, 1, D, views=views, device=local)
+    sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -187,6 +196,10 @@ def main():
             # the 8-path aggregation kernels (everything after the cost volume
             # except vfwd, which is mostly the vertical cost filter)
             agg = [k for k in kernels if k.startswith(("sweep_", "pair_", "stage_"))]
+            post = [k for k in kernels if k.startswith("post_")]
+            if post:
+                roofline["post_filter_ms_per_step"] = round(
+                    sum(kernels[k]["share_per_step_ms"] for k in post), 4)
             agg_ms = sum(kernels[k]["share_per_step_ms"] for k in agg)
             if agg_ms > 0:
                 agg_bytes = sum(kernels[k]["algo_bytes"] * kernels[k]["launches"] / args.steps
@@ -239,8 +252,9 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": cfg["workload"], "width": w, "height": h, "max_disp": D,
-                       "views": views, "pairs_per_gpu": 1, "global_batch": world,
+            "config": {"workload": cfg["workload"] + (" + post_filter" if args.post_filter else ""),
+                       "width": w, "height": h, "max_disp": D, "views": views,
+                       "post_filter": bool(args.post_filter), "pairs_per_gpu": 1, "global_batch": world,
                        "parallelism": f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
             "host_io": host_io,

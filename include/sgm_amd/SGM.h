@@ -203,6 +203,7 @@ public:
     explicit SGM(int h, int w, int s, int d) : Solver(h, w, s, d) {
         sgm_params p;
         if (sgm_default_params(&p, h, w, s, d) != SGM_OK) fail("SGM", "sgm_default_params");
+        p.post_filter = 1;  // process() ends with post_filter(), SGM.cpp:821 (on the GPU)
         const int rc = sgm_create(&p, device(), &handle_);
         if (rc != SGM_OK) fail("SGM: sgm_create", handle_ ? sgm_last_error(handle_) : "no device");
     }
@@ -213,7 +214,7 @@ public:
     SGM(const SGM &) = delete;
     SGM &operator=(const SGM &) = delete;
 
-    // SGM.cpp:32-826: both views, LR check, then post_filter() (:821)
+    // SGM.cpp:32-826: both views, LR check, then post_filter() (:821), all on the GPU
     virtual void process(Mat &img_l, Mat &img_r) {
         if (img_l.rows != img_r.rows || img_l.cols != img_r.cols || img_l.type() != img_r.type() ||
             img_l.type() != CV_8UC1 || img_l.rows != in_h_ || img_l.cols != in_w_)
@@ -232,9 +233,6 @@ public:
                                    (int)(filtered_disp.step / sizeof(float)), nullptr);
         if (rc != SGM_OK) fail("SGM::process", sgm_last_error(handle_));
         if (scale > 1) decimate_left();
-        if (sgm_post_filter_host(filtered_disp.template ptr<float>(0), img_h, img_w, max_disp,
-                                 scale) != SGM_OK)
-            fail("SGM::process", "post_filter");
     }
     // SGM.cpp:829-834
     virtual void process(Mat &img_l, Mat &img_r, Mat &sky_mask, Mat &sky_mask_beta) {

@@ -64,6 +64,9 @@ typedef struct sgm_params {
     float lr_max_diff; /* 1.0 LR_CHECK_DIS (inc/Solver.h:16) */
     int blur;          /* 1: pre-blur as Solver.cpp:124-125 (pinned formula); 0: off */
     int views;         /* 2: left+right views + LR check (SGM.cpp:32-818); 1: left view only */
+    int post_filter;   /* 1: sgm_process[_device] output is post_filter()ed on the GPU
+                          (Solver.cpp:600-649, what get_disp() returns, SGM.cpp:821);
+                          0 (default): the LR-checked map (filtered_disp at SGM.cpp:818) */
 } sgm_params;
 
 typedef struct sgm_handle sgm_handle;
@@ -89,7 +92,9 @@ size_t sgm_device_bytes(const sgm_handle *h);
  *                NULL (Solver.cpp:146)
  *   out        : f32 rows x cols, LR-checked sub-pixel disparity
  *                (filtered_disp after SGM.cpp:818), invalid = D+1; with
- *                views == 1 it is the left sub-pixel map (SGM.cpp:443)
+ *                params.post_filter it is then post_filter()ed on the GPU
+ *                (SGM.cpp:821, what get_disp() returns); with views == 1 it
+ *                is the left sub-pixel map (SGM.cpp:443)
  *   raw_disp   : optional u16 rows x cols, left WTA disparity (SGM.cpp:411-415)
  */
 int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
@@ -97,15 +102,26 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
                 float *out, int out_pitch, uint16_t *raw_disp);
 
 /* Same on DEVICE buffers, enqueued on `stream` (a hipStream_t; NULL = the
- * handle's own stream).  Returns after enqueueing; the caller synchronises. */
+ * handle's own stream).  Returns after enqueueing; the caller synchronises.
+ * With params.post_filter the call synchronises `stream` during the median
+ * fill's convergence test (sgm_post_filter_device). */
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
                        float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream);
 
 /* post_filter() (Solver.cpp:600-649) on a host rows x cols f32 map, in place:
- * 5x5 median fill + speckle removal, single-thread semantics.  Runs on the
- * host (outside the north-star hot path). */
+ * 5x5 median fill + speckle removal, single-thread semantics, on the host CPU
+ * (kept for callers without a handle; the GPU entry points below replace it). */
 int sgm_post_filter_host(float *disp, int rows, int cols, int max_disp, int scale);
+
+/* post_filter() (Solver.cpp:600-649: median fill :604-630, speckle_filter_new
+ * :514-566) on the GPU, bit-exact against its single-thread semantics, in
+ * place on a DEVICE map of the handle's working size (rows x cols f32, row
+ * pitch in floats), enqueued on `stream` (NULL = the handle's stream).  The
+ * median fill iterates to a proven fixed point; the call synchronises
+ * `stream` once per two fill launches to read the convergence counter, and
+ * returns with the speckle kernels enqueued (the caller synchronises). */
+int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream);
 
 /* ---- per-kernel timing (HIP events recorded around every launch) ---- */
 
@@ -141,6 +157,9 @@ int sgm_stage_path(sgm_handle *h, int dir, const float *cost, float *L, float *m
 int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float *sub);
 /* LR check (SGM.cpp:803-818): out = checked copy of fl. */
 int sgm_stage_lr(sgm_handle *h, const float *fl, const float *fr, float *out);
+/* post_filter() (Solver.cpp:600-649) on a HOST rows x cols map, in place,
+ * computed on the GPU (sgm_post_filter_device); synchronous. */
+int sgm_stage_post_filter(sgm_handle *h, float *disp);
 
 #ifdef __cplusplus
 }

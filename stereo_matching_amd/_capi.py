@@ -23,8 +23,9 @@ SGM_ERR_NO_DEVICE = 4
 EXPORTS = (
     "sgm_default_params", "sgm_create", "sgm_destroy", "sgm_last_error", "sgm_get_size",
     "sgm_device_bytes", "sgm_process", "sgm_process_device", "sgm_post_filter_host",
-    "sgm_stage_census", "sgm_stage_cost", "sgm_stage_path", "sgm_stage_aggregate",
-    "sgm_stage_lr", "sgm_set_profiling", "sgm_get_profile",
+    "sgm_post_filter_device", "sgm_stage_census", "sgm_stage_cost", "sgm_stage_path",
+    "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
+    "sgm_get_profile",
 )
 
 
@@ -39,7 +40,7 @@ class Params(ctypes.Structure):
         ("height", ctypes.c_int), ("width", ctypes.c_int), ("scale", ctypes.c_int),
         ("max_disp", ctypes.c_int), ("p1", ctypes.c_int), ("p2", ctypes.c_int),
         ("uniqueness", ctypes.c_float), ("lr_max_diff", ctypes.c_float),
-        ("blur", ctypes.c_int), ("views", ctypes.c_int),
+        ("blur", ctypes.c_int), ("views", ctypes.c_int), ("post_filter", ctypes.c_int),
     ]
 
 
@@ -82,6 +83,8 @@ def lib():
     L.sgm_process.argtypes = [P, P, P, I, P, P, I, P, I, P]
     L.sgm_process_device.argtypes = [P, P, P, I, P, P, I, P, I, P, P]
     L.sgm_post_filter_host.argtypes = [P, I, I, I, I]
+    L.sgm_post_filter_device.argtypes = [P, P, I, P]
+    L.sgm_stage_post_filter.argtypes = [P, P]
     L.sgm_stage_census.argtypes = [P, P, I, P]
     L.sgm_stage_cost.argtypes = [P, P, P, P, I, I, P]
     L.sgm_stage_path.argtypes = [P, I, P, P, P]

@@ -49,6 +49,16 @@ struct sgm_handle {
     float *d_min;         // minL (stage_path)
     float *d_zero;        // 256 zero floats (PairArgs::zero)
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
+    // post_filter scratch (sgm_post.hip)
+    float *d_pf_orig;     // the map as it entered the median fill
+    float *d_pf_work;     // contiguous working map (pitched callers)
+    int *d_pf_label;      // union-find parents
+    int *d_pf_count;      // pixels under each tile-local root
+    int *d_pf_area;       // component sizes
+    float *d_pf_snap;     // per median tile: the working-map cells it last read
+    int *d_pf_changes;    // per median launch: tiles that changed a pixel
+    int *h_pf_changes;    // pinned readback of one counter
+    int pf_iters;         // median launches of the last post filter
     uint8_t *h_pin;       // pinned host staging for sgm_process (allocated on first use)
     size_t h_pin_bytes;
     char err[512];
@@ -130,6 +140,11 @@ void free_all(sgm_handle *h) {
         (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
     }
     (void)hipFree(h->d_out);
+    (void)hipFree(h->d_pf_orig); (void)hipFree(h->d_pf_work); (void)hipFree(h->d_pf_label);
+    (void)hipFree(h->d_pf_count); (void)hipFree(h->d_pf_area); (void)hipFree(h->d_pf_snap);
+    (void)hipFree(h->d_pf_changes);
+    if (h->h_pf_changes) (void)hipHostFree(h->h_pf_changes);
+    h->h_pf_changes = nullptr;
     (void)hipFree(h->d_min);
     (void)hipFree(h->d_zero);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -180,6 +195,10 @@ hipError_t timed(sgm_handle *h, const char *name, double elems, hipStream_t st, 
     h->pending.push_back({stat_class(h, name, elems), a, b});
     return e;
 }
+
+// Upper bound on median-fill launches of one post filter: the fill reaches its
+// fixed point in 2-3 launches on stereo output; the bound only stops a runaway.
+constexpr int kMedianMaxLaunches = 4096;
 
 const char *kDirName[8] = {"L1", "L2", "L3", "L4", "L5", "L6", "L7", "L8"};
 const char *kModeName[4] = {"store", "init", "acc", "final"};
@@ -284,6 +303,8 @@ int cost_view(sgm_handle *h, int view, const uint8_t *sky, int sky_pitch, hipStr
     return SGM_OK;
 }
 
+int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st);
+
 int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
               const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch, float *d_out,
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
@@ -331,6 +352,8 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     if (d_raw)
         HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
                                  hipMemcpyDeviceToDevice, st));
+    if (h->p.post_filter)  // SGM.cpp:821
+        return post_filter(h, d_out, out_pitch, st);
     return SGM_OK;
 }
 
@@ -363,6 +386,55 @@ void pack_rows(uint8_t *dst, const uint8_t *src, size_t row_bytes, int rows, siz
     for (int i = 0; i < rows; ++i) memcpy(dst + i * row_bytes, src + i * pitch, row_bytes);
 }
 
+// post_filter() (Solver.cpp:600-649) in place on a device map (sgm_post.hip):
+// median-fill launches until one changes nothing, then the speckle removal.
+int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
+    const Geom g = h->g;
+    const size_t npx = (size_t)g.H * g.W, row = (size_t)g.W * sizeof(float);
+    const double dnpx = (double)npx;
+    float *F = pitch == g.W ? d_map : h->d_pf_work;
+    HIPCHK(h, hipMemcpy2DAsync(h->d_pf_orig, row, d_map, (size_t)pitch * sizeof(float), row, g.H,
+                               hipMemcpyDeviceToDevice, st));
+    if (F != d_map)
+        HIPCHK(h, hipMemcpyAsync(F, h->d_pf_orig, npx * sizeof(float), hipMemcpyDeviceToDevice, st));
+    HIPCHK(h, hipMemsetAsync(h->d_pf_changes, 0, kMedianMaxLaunches * sizeof(int), st));
+    int k = 0;
+    for (;;) {
+        // a fill usually settles in 2 launches and the 3rd proves it
+        const int batch = k == 0 ? 3 : 2;
+        for (int b = 0; b < batch; ++b, ++k)
+            HIPCHK(h, timed(h, "post_median", dnpx, st, [&] {
+                       return sgm::launch_median_fill(h->d_pf_orig, F, k, h->d_pf_snap,
+                                                      h->d_pf_changes, g, st);
+                   }));
+        HIPCHK(h, hipMemcpyAsync(h->h_pf_changes, h->d_pf_changes + k - 1, sizeof(int),
+                                 hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        if (*h->h_pf_changes == 0) break;
+        if (k + 3 > kMedianMaxLaunches)
+            return set_err(h, SGM_ERR_HIP, "post_filter: median fill did not converge in %d launches",
+                           k);
+    }
+    h->pf_iters = k;
+    HIPCHK(h, timed(h, "post_cc_local", dnpx, st,
+                    [&] { return sgm::launch_cc_local(F, h->d_pf_label, h->d_pf_count, g, st); }));
+    HIPCHK(h, timed(h, "post_cc_merge", dnpx, st,
+                    [&] { return sgm::launch_cc_merge(F, h->d_pf_label, g, st); }));
+    HIPCHK(h, hipMemsetAsync(h->d_pf_area, 0, npx * sizeof(int), st));
+    HIPCHK(h, timed(h, "post_cc_count", dnpx, st, [&] {
+               return sgm::launch_cc_count(h->d_pf_label, h->d_pf_count, h->d_pf_area, g, st);
+           }));
+    // speckle_filter_new(filtered_disp, invalid_disp, SPECKLE_SIZE/scale, SPECKLE_DIS), :645
+    HIPCHK(h, timed(h, "post_cc_apply", dnpx, st, [&] {
+               return sgm::launch_cc_apply(F, h->d_pf_label, h->d_pf_area, 1000 / g.scale,
+                                           (float)(g.D + 1), g, st);
+           }));
+    if (F != d_map)
+        HIPCHK(h, hipMemcpy2DAsync(d_map, (size_t)pitch * sizeof(float), F, row, row, g.H,
+                                   hipMemcpyDeviceToDevice, st));
+    return SGM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -379,6 +451,7 @@ int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
     p->lr_max_diff = 1.0f;   // inc/Solver.h:16
     p->blur = 1;             // Solver.cpp:124-125
     p->views = 2;            // SGM.cpp:448-818
+    p->post_filter = 0;      // out = LR-checked map (SGM.cpp:818); 1: + post_filter (:821)
     return SGM_OK;
 }
 
@@ -447,6 +520,16 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         if (!rc) rc = dalloc(h, &h->d_out, npx);
         if (!rc) rc = dalloc(h, &h->d_min, npx);
         if (!rc) rc = dalloc(h, &h->d_zero, 256);
+        if (!rc) rc = dalloc(h, &h->d_pf_orig, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_work, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_label, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_count, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_area, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_snap, sgm::post_snapshot_floats(h->g));
+        if (!rc) rc = dalloc(h, &h->d_pf_changes, (size_t)kMedianMaxLaunches);
+        if (!rc && hipHostMalloc((void **)&h->h_pf_changes, sizeof(int), hipHostMallocDefault) !=
+                       hipSuccess)
+            rc = set_err(h, SGM_ERR_HIP, "hipHostMalloc of the post-filter counter failed");
         if (!rc && hipMemset(h->d_zero, 0, 256 * sizeof(float)) != hipSuccess)
             rc = set_err(h, SGM_ERR_HIP, "hipMemset of the zero page failed");
     } while (0);
@@ -684,6 +767,26 @@ int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float 
     if (rc) return rc;
     if (disp) HIPCHK(h, hipMemcpyAsync(disp, h->d_disp[0], npx * 2, hipMemcpyDeviceToHost, h->st));
     if (sub) HIPCHK(h, hipMemcpyAsync(sub, h->d_sub[0], npx * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!d_disp || pitch < h->g.W)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_post_filter_device: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    return post_filter(h, d_disp, pitch, stream ? (hipStream_t)stream : h->st);
+}
+
+int sgm_stage_post_filter(sgm_handle *h, float *disp) {
+    if (!h || !disp) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    HIPCHK(h, hipMemcpyAsync(h->d_out, disp, npx * 4, hipMemcpyHostToDevice, h->st));
+    int rc = post_filter(h, h->d_out, h->g.W, h->st);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(disp, h->d_out, npx * 4, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return SGM_OK;
 }

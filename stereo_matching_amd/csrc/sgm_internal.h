@@ -85,6 +85,15 @@ hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t
                          hipStream_t st);
 hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st);
 hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream_t st);
+// post_filter (sgm_post.hip)
+size_t post_snapshot_floats(Geom g);
+hipError_t launch_median_fill(const float *orig, float *F, int iter, float *snap, int *changes,
+                              Geom g, hipStream_t st);
+hipError_t launch_cc_local(const float *F, int *L, int *cnt, Geom g, hipStream_t st);
+hipError_t launch_cc_merge(const float *F, int *L, Geom g, hipStream_t st);
+hipError_t launch_cc_count(int *L, const int *cnt, int *area, Geom g, hipStream_t st);
+hipError_t launch_cc_apply(float *F, const int *L, const int *area, int max_size, float value,
+                           Geom g, hipStream_t st);
 hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
                      Geom g, hipStream_t st);
 

@@ -35,11 +35,14 @@ class SGM:
 
     def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0,
                  blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
-                 uniqueness: float = 0.7, lr_max_diff: float = 1.0):
+                 uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False):
         self._lib = lib()
         p = _capi.default_params(h, w, s, d)
         p.blur = int(bool(blur))
         p.views = views
+        # post_filter: process_device's output is post_filter()ed on the GPU
+        # (SGM.cpp:821); process() keeps the LR map and get_disp() filters it
+        p.post_filter = int(bool(post_filter))
         p.p1, p.p2 = p1, p2
         p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
         self.params = p
@@ -89,6 +92,8 @@ class SGM:
                                     self.cols, _ptr(self._lr), self.cols, _ptr(self._raw)),
               self._h)
         self._final = None
+        if self.params.post_filter:  # sgm_process returned get_disp() itself
+            self._final, self._lr = self._lr, None
 
     def process_device(self, d_left: int, d_right: int, d_out: int, *, pitch: int | None = None,
                        d_sky_l: int = 0, d_sky_r: int = 0, sky_pitch: int | None = None,
@@ -102,17 +107,31 @@ class SGM:
 
     def get_disp(self) -> np.ndarray:
         """Post-filtered disparity (inc/Solver.h:36: filtered_disp after
-        post_filter, Solver.cpp:600-649); invalid = D+1."""
+        post_filter, Solver.cpp:600-649), computed on the GPU; invalid = D+1."""
         if self._final is None:
-            f = self._lr.copy()
-            check(self._lib.sgm_post_filter_host(_ptr(f), self.rows, self.cols, self.max_disp,
-                                                 self.scale))
-            self._final = f
+            self._final = self.post_filter(self._lr)
         return self._final
 
     def get_lr_disp(self) -> np.ndarray:
         """Sub-pixel disparity after the LR check (SGM.cpp:803-818)."""
+        if self._lr is None:
+            raise RuntimeError("constructed with post_filter=True: only get_disp() is kept")
         return self._lr
+
+    def post_filter(self, disp) -> np.ndarray:
+        """post_filter() (Solver.cpp:600-649) of a rows x cols map on the GPU
+        (sgm_stage_post_filter); returns a filtered copy."""
+        f = np.array(disp, dtype=np.float32, copy=True, order="C")
+        if f.shape != (self.rows, self.cols):
+            raise ValueError(f"disp: expected shape {(self.rows, self.cols)}, got {f.shape}")
+        check(self._lib.sgm_stage_post_filter(self._h, _ptr(f)), self._h)
+        return f
+
+    def post_filter_device(self, d_disp: int, *, pitch: int | None = None, stream: int = 0) -> None:
+        """In place on a device map (sgm_post_filter_device)."""
+        check(self._lib.sgm_post_filter_device(self._h, ctypes.c_void_p(d_disp),
+                                               pitch or self.cols,
+                                               ctypes.c_void_p(stream or None)), self._h)
 
     def get_raw_disp(self) -> np.ndarray:
         """Left WTA disparity (SGM.cpp:411-415), uint16, invalid = D+1."""

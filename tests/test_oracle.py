@@ -264,3 +264,36 @@ def test_oracle_against_golden(name):
     for k in range(8):
         L, _ = oracle.path(cost, k)
         assert hashlib.sha256(L.tobytes()).hexdigest() == hashes[f"L{k + 1}"], k
+
+
+@pytest.mark.parametrize("kind", __import__("postfilter_maps").KINDS)
+def test_post_filter_oracle_vs_numpy_on_stress_maps(kind):
+    # the oracle's sequential median fill + component test against the
+    # independent numpy restatement, on the maps the GPU parity tests use
+    import postfilter_maps
+    for (H, W, D, s) in ((40, 90, 64, 1), (23, 70, 32, 2)):
+        F = postfilter_maps.make(kind, H, W, D, 1)
+        got = oracle.post_filter(F.copy(), D, s)
+        want = pyref.post_filter(F, D, s)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (kind, H, W)
+
+
+def test_post_filter_median_fill_is_sequential():
+    # Known answer: the in-place raster order of Solver.cpp:604-630.  Row 5
+    # holds an invalid run; (5, 3) is filled first and its value joins the
+    # window of (5, 4), so the run fills left to right from earlier fills.
+    # 40x40 (one component of 1600 > 1000 pixels, so the speckle pass keeps it)
+    D = 64
+    F = np.zeros((40, 40), np.float32)
+    F[:, :] = np.arange(40, dtype=np.float32)[None, :]   # column index as disparity
+    F[5, 2:9] = D + 1
+    out = oracle.post_filter(F.copy(), D)
+    assert np.array_equal(out.view(np.uint32), pyref.post_filter(F, D).view(np.uint32))
+    # (5,2): 4 full rows {0..4} + (5,0), (5,1) = 22 samples, v[11] = 2; (5,3)
+    # then sees the fill 2 at (5,2): {1..5}x4 + {1, 2}, v[11] = 3; and so on
+    assert np.array_equal(out[5, 2:9], np.arange(2, 9, dtype=np.float32))
+    # a second run right below: row 5's fills are in row 6's windows
+    G = F.copy()
+    G[6, 3:6] = D + 1
+    out = oracle.post_filter(G.copy(), D)
+    assert np.array_equal(out.view(np.uint32), pyref.post_filter(G, D).view(np.uint32))
