@@ -76,7 +76,9 @@ BYTES_PER_PIXEL = {"census": 9, "lr": 12,
                    # writes label + count (12); the area test reads map, 2 labels,
                    # area and writes the map (16); count/merge touch few pixels
                    "post_median": 8, "post_cc_local": 12, "post_cc_apply": 16,
-                   "post_cc_count": 4, "post_cc_merge": 0}
+                   "post_cc_count": 4, "post_cc_merge": 0,
+                   # LKRefine: map in + out, 7x7 window and images through LDS/L2
+                   "lk_refine": 10}
 
 
 def algorithmic_bytes(name: str, elems: float, D: int) -> float:
@@ -98,6 +100,8 @@ def parse():
     ap.add_argument("--no-profile-pass", action="store_true")
     ap.add_argument("--post-filter", action="store_true",
                     help="end each step with post_filter() on the GPU (SGM.cpp:821; V=2 configs)")
+    ap.add_argument("--lk-refine", action="store_true",
+                    help="end each step with LKRefine on the GPU (SGM.cpp:824, LKSubPixelImpl.cpp)")
     ap.add_argument("--host-io", action="store_true",
                     help="also time sgm_process on host buffers (PCIe-inclusive, not `value`)")
     return ap.parse_args()
@@ -130,7 +134,8 @@ def main():
     d_out = torch.empty((h, w), dtype=torch.float32, device=dev)
     gather = [torch.empty_like(d_out) for _ in range(world)] if (world > 1 and rank == 0) else None
 
-    sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter)
+    sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter,
+              lk_refine=args.lk_refine)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -252,9 +257,10 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": cfg["workload"] + (" + post_filter" if args.post_filter else ""),
+            "config": {"workload": cfg["workload"] + (" + post_filter" if args.post_filter else "")
+                       + (" + LKRefine" if args.lk_refine else ""),
                        "width": w, "height": h, "max_disp": D, "views": views,
-                       "post_filter": bool(args.post_filter), "pairs_per_gpu": 1, "global_batch": world,
+                       "post_filter": bool(args.post_filter), "lk_refine": bool(args.lk_refine), "pairs_per_gpu": 1, "global_batch": world,
                        "parallelism": f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
             "host_io": host_io,

@@ -67,6 +67,8 @@ typedef struct sgm_params {
     int post_filter;   /* 1: sgm_process[_device] output is post_filter()ed on the GPU
                           (Solver.cpp:600-649, what get_disp() returns, SGM.cpp:821);
                           0 (default): the LR-checked map (filtered_disp at SGM.cpp:818) */
+    int lk_refine;     /* 1: then LKRefine on the GPU (LKSubPixelImpl.cpp:13-235; the call
+                          at SGM.cpp:824 is commented out in the reference); 0 (default) */
 } sgm_params;
 
 typedef struct sgm_handle sgm_handle;
@@ -123,6 +125,18 @@ int sgm_post_filter_host(float *disp, int rows, int cols, int max_disp, int scal
  * returns with the speckle kernels enqueued (the caller synchronises). */
 int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream);
 
+/* LKSubPixelImpl::LKRefine(img_l, img_r, disp_float) (LKRefine/LKSubPixelImpl.cpp:
+ * 13-235) on the GPU: per-pixel Gauss-Newton refinement of the disparity over
+ * a 7x7 window, interior pixels truncated first (:80), border pixels untouched.
+ * d_left/d_right: DEVICE u8 images at the handle's full size (height x width,
+ * row pitch in bytes), decimated by the scale as :29-44 does; d_disp: DEVICE
+ * working-grid map (rows x cols f32, pitch in floats), refined in place.
+ * Enqueued on `stream` (NULL = the handle's stream); the caller synchronises.
+ * fp32 sums follow oracle/sgm_oracle.c:orc_lk_refine bit-for-bit (the
+ * reference's Eigen reduction order is not pinned). */
+int sgm_lk_refine_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+                         float *d_disp, int disp_pitch, void *stream);
+
 /* ---- per-kernel timing (HIP events recorded around every launch) ---- */
 
 typedef struct sgm_kernel_stat {
@@ -160,6 +174,10 @@ int sgm_stage_lr(sgm_handle *h, const float *fl, const float *fr, float *out);
 /* post_filter() (Solver.cpp:600-649) on a HOST rows x cols map, in place,
  * computed on the GPU (sgm_post_filter_device); synchronous. */
 int sgm_stage_post_filter(sgm_handle *h, float *disp);
+/* LKRefine (sgm_lk_refine_device) with HOST buffers: left/right full-size u8
+ * images (pitch bytes), disp a rows x cols map refined in place; synchronous. */
+int sgm_stage_lk_refine(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
+                        float *disp);
 
 #ifdef __cplusplus
 }

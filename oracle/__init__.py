@@ -55,6 +55,7 @@ def lib():
         L.orc_subpixel.argtypes = [P, P, P, I, I, I]
         L.orc_lr_check.argtypes = [P, P, I, I, I, I, F]
         L.orc_post_filter.argtypes = [P, I, I, I, I]
+        L.orc_lk_refine.argtypes = [P, P, P, I, I, I]
         L.orc_process.argtypes = [P, P, P, P, I, I, I, I, I, I, F, F, I, I, ctypes.POINTER(_Result)]
         L.orc_process.restype = I
         L.orc_max_threads.restype = I
@@ -156,6 +157,18 @@ def post_filter(F, D, scale=1):
     F = np.array(F, dtype=np.float32, copy=True, order="C")
     H, W = F.shape
     lib().orc_post_filter(_p(F), H, W, D, scale)
+    return F
+
+
+def lk_refine(left, right, disp, D):
+    """LKRefine (LKSubPixelImpl.cpp:13-235) on working-grid images; returns a
+    refined copy of disp."""
+    L = _c(left, np.uint8)
+    R = _c(right, np.uint8)
+    F = np.array(disp, np.float32, copy=True, order="C")
+    H, W = F.shape
+    assert L.shape == R.shape == (H, W)
+    lib().orc_lk_refine(_p(L), _p(R), _p(F), H, W, D)
     return F
 
 

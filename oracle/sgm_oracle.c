@@ -455,6 +455,98 @@ void orc_post_filter(float *F, int H, int W, int D, int scale)
     free(area);
 }
 
+/* ---------------------------------------------------------- LK refine */
+
+/* LKSubPixelImpl::LKRefine + LKRefineCore (LKRefine/LKSubPixelImpl.cpp:13-235,
+ * constants LKSubPixelImpl.h:31-48: win_size 7, iter_num 10, GradValid
+ * g > 2, DispValid 0 < d < max_disp).  L, R: working-grid images (the caller
+ * decimates, :29-44); disp: working-grid float map, refined in place.
+ *
+ * The reference's linear algebra is Eigen (third-party, not in this image);
+ * its 1x1 products are restated as plain fp32 sums in index order k = 0..48,
+ * evaluated the way its expression groups them:
+ *   Hessian = (J^T * W) * J        -> sum_k (Ix_k * w_k) * Ix_k         (:176)
+ *   doff    = ((H^-1 * J^T) * W) * r -> sum_k ((hinv * Ix_k) * w_k) * r_k (:185)
+ *   w       = w / ||w||            -> w_k / sqrtf(sum_k w_k * w_k)       (:172)
+ * Eigen's vectorised reductions may sum in another order; that order is not
+ * pinned (no reference output exists), the GPU matches this one bit-for-bit.
+ * Slots with zero weight leave win_Ix / win_Ires uninitialised in the
+ * reference (:117-160); they are 0 here. */
+void orc_lk_refine(const uint8_t *L, const uint8_t *R, float *disp, int H, int W, int D)
+{
+    const int hw = 3, win = 7, iters = 10;
+    const i64 n = (i64)H * W;
+    float *Ix = (float *)calloc((size_t)n, sizeof(float));
+    float *dt = (float *)malloc(sizeof(float) * (size_t)n);
+    float *nd = (float *)malloc(sizeof(float) * (size_t)n);
+    memcpy(dt, disp, sizeof(float) * (size_t)n);
+    memcpy(nd, disp, sizeof(float) * (size_t)n);
+    /* gradients + integer truncation of the interior (:70-82) */
+    for (int i = hw; i < H - hw; ++i)
+        for (int j = hw; j < W - hw; ++j) {
+            const i64 k = (i64)i * W + j;
+            Ix[k] = (float)((int)L[k + 1] - (int)L[k - 1]) * 0.5f;
+            nd[k] = (float)(int)disp[k];
+            dt[k] = (float)(int)disp[k];
+        }
+    /* per-pixel Gauss-Newton on the disparity offset (:86-233) */
+    for (int i = hw; i < H - hw; ++i) {
+        for (int j = hw; j < W - hw; ++j) {
+            const i64 c = (i64)i * W + j;
+            if (!(Ix[c] > 2)) continue;
+            const float d0 = dt[c];
+            if (!(d0 > 0 && d0 < D)) continue;
+            float last_disp = d0, last_doff = 0.f, last_diff = FLT_MAX;
+            for (int it = 0; it < iters; ++it) {
+                float w[49], jx[49], res[49];
+                int cnt = 0, valid = 0;
+                for (int v = -hw; v <= hw; ++v)
+                    for (int u = -hw; u <= hw; ++u, ++cnt) {
+                        const int m = i + v, nn = j + u;
+                        const i64 k = (i64)m * W + nn;
+                        w[cnt] = 0.f;
+                        jx[cnt] = 0.f;
+                        res[cnt] = 0.f;
+                        if (!(Ix[k] > 2)) continue;
+                        const float dm = dt[k];
+                        if (!(dm > 0 && dm < D)) continue;
+                        if (fabsf(d0 - dm) > 2) continue;
+                        const float dw = dm + last_doff;
+                        if ((float)nn - dw < 0 || (float)nn - dw > (float)(W - 1)) continue;
+                        /* exp of an int: -(v^2+u^2)/(2*3*3) is 0 or -1 (:154) */
+                        w[cnt] = (float)exp((double)(-(v * v + u * u) / (2 * hw * hw)));
+                        res[cnt] = (float)((int)R[(i64)m * W + (int)((float)nn - dw)] - (int)L[k]);
+                        jx[cnt] = Ix[k];
+                        ++valid;
+                    }
+                if (valid < win * win * 0.1) break;                    /* :165 */
+                float s2 = 0.f;
+                for (int k = 0; k < 49; ++k) s2 += w[k] * w[k];
+                const float nrm = sqrtf(s2);
+                for (int k = 0; k < 49; ++k) w[k] = w[k] / nrm;
+                float hs = 0.f;
+                for (int k = 0; k < 49; ++k) hs += (jx[k] * w[k]) * jx[k];
+                if (isnan(hs) || (double)hs < 1e-3) break;               /* :178 */
+                const float hinv = 1.0f / hs;
+                float doff = 0.f;
+                for (int k = 0; k < 49; ++k) doff += ((hinv * jx[k]) * w[k]) * res[k];
+                if (isnan(doff)) break;                                /* :188 */
+                if (fabsf(doff - last_doff) > last_diff) break;        /* :201 */
+                if (!(d0 + doff > 0 && d0 + doff < D)) break;          /* :207 */
+                last_disp = d0 + doff;
+                last_diff = fabsf(doff - last_doff);
+                last_doff = doff;
+                if ((double)last_diff < 1e-6) break;                   /* :222 */
+            }
+            nd[c] = last_disp;
+        }
+    }
+    memcpy(disp, nd, sizeof(float) * (size_t)n);
+    free(Ix);
+    free(dt);
+    free(nd);
+}
+
 /* --------------------------------------------------------- whole process */
 
 int orc_process(const uint8_t *left, const uint8_t *right,

@@ -79,6 +79,11 @@ void orc_lr_check(float *FL, const float *FR, int H, int W, int D, int scale, fl
  * (speckle_filter_new, Solver.cpp:514-566) with its single-thread semantics. */
 void orc_post_filter(float *F, int H, int W, int D, int scale);
 
+/* LKRefine (LKRefine/LKSubPixelImpl.cpp:13-235) on working-grid images L, R
+ * and a working-grid disparity map (refined in place); see sgm_oracle.c for
+ * the pinned fp32 evaluation order of its Eigen expressions. */
+void orc_lk_refine(const uint8_t *L, const uint8_t *R, float *disp, int H, int W, int D);
+
 typedef struct orc_result {
     /* all optional (NULL = not wanted); sizes use the working (decimated) h, w */
     int32_t *disp;          /* left WTA disparity, HW */

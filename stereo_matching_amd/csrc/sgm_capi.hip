@@ -59,6 +59,7 @@ struct sgm_handle {
     int *d_pf_changes;    // per median launch: tiles that changed a pixel
     int *h_pf_changes;    // pinned readback of one counter
     int pf_iters;         // median launches of the last post filter
+    float *d_lk_in;       // LKRefine input copy (the kernel refines the map in place)
     uint8_t *h_pin;       // pinned host staging for sgm_process (allocated on first use)
     size_t h_pin_bytes;
     char err[512];
@@ -143,6 +144,7 @@ void free_all(sgm_handle *h) {
     (void)hipFree(h->d_pf_orig); (void)hipFree(h->d_pf_work); (void)hipFree(h->d_pf_label);
     (void)hipFree(h->d_pf_count); (void)hipFree(h->d_pf_area); (void)hipFree(h->d_pf_snap);
     (void)hipFree(h->d_pf_changes);
+    (void)hipFree(h->d_lk_in);
     if (h->h_pf_changes) (void)hipHostFree(h->h_pf_changes);
     h->h_pf_changes = nullptr;
     (void)hipFree(h->d_min);
@@ -304,6 +306,8 @@ int cost_view(sgm_handle *h, int view, const uint8_t *sky, int sky_pitch, hipStr
 }
 
 int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st);
+int lk_refine(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+              float *d_map, int map_pitch, hipStream_t st);
 
 int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
               const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch, float *d_out,
@@ -352,8 +356,10 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     if (d_raw)
         HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
                                  hipMemcpyDeviceToDevice, st));
-    if (h->p.post_filter)  // SGM.cpp:821
-        return post_filter(h, d_out, out_pitch, st);
+    if (h->p.post_filter && (rc = post_filter(h, d_out, out_pitch, st)))  // SGM.cpp:821
+        return rc;
+    if (h->p.lk_refine)  // SGM.cpp:824
+        return lk_refine(h, d_left, d_right, pitch, d_out, out_pitch, st);
     return SGM_OK;
 }
 
@@ -435,6 +441,21 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
     return SGM_OK;
 }
 
+// LKRefine (sgm_lk.hip) in place on a device map: the kernel reads a
+// contiguous copy of the map and writes the refined values back.
+int lk_refine(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+              float *d_map, int map_pitch, hipStream_t st) {
+    const Geom g = h->g;
+    const size_t row = (size_t)g.W * sizeof(float);
+    HIPCHK(h, hipMemcpy2DAsync(h->d_lk_in, row, d_map, (size_t)map_pitch * sizeof(float), row, g.H,
+                               hipMemcpyDeviceToDevice, st));
+    HIPCHK(h, timed(h, "lk_refine", (double)g.H * g.W, st, [&] {
+               return sgm::launch_lk_refine(d_left, d_right, pitch, h->d_lk_in, d_map, map_pitch, g,
+                                            st);
+           }));
+    return SGM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -452,6 +473,7 @@ int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
     p->blur = 1;             // Solver.cpp:124-125
     p->views = 2;            // SGM.cpp:448-818
     p->post_filter = 0;      // out = LR-checked map (SGM.cpp:818); 1: + post_filter (:821)
+    p->lk_refine = 0;        // 1: + LKRefine (SGM.cpp:824, commented out in the reference)
     return SGM_OK;
 }
 
@@ -526,6 +548,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         if (!rc) rc = dalloc(h, &h->d_pf_count, npx);
         if (!rc) rc = dalloc(h, &h->d_pf_area, npx);
         if (!rc) rc = dalloc(h, &h->d_pf_snap, sgm::post_snapshot_floats(h->g));
+        if (!rc) rc = dalloc(h, &h->d_lk_in, npx);
         if (!rc) rc = dalloc(h, &h->d_pf_changes, (size_t)kMedianMaxLaunches);
         if (!rc && hipHostMalloc((void **)&h->h_pf_changes, sizeof(int), hipHostMallocDefault) !=
                        hipSuccess)
@@ -777,6 +800,31 @@ int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_post_filter_device: bad pointer or pitch");
     DeviceGuard guard(h->device);
     return post_filter(h, d_disp, pitch, stream ? (hipStream_t)stream : h->st);
+}
+
+int sgm_lk_refine_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+                         float *d_disp, int disp_pitch, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!d_left || !d_right || !d_disp || pitch < h->p.width || disp_pitch < h->g.W)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_lk_refine_device: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    return lk_refine(h, d_left, d_right, pitch, d_disp, disp_pitch,
+                     stream ? (hipStream_t)stream : h->st);
+}
+
+int sgm_stage_lk_refine(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
+                        float *disp) {
+    if (!h || !left || !right || !disp || pitch < h->p.width) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    int rc;
+    if ((rc = copy_in_image(h, h->d_in[0], left, pitch))) return rc;
+    if ((rc = copy_in_image(h, h->d_in[1], right, pitch))) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->d_out, disp, npx * 4, hipMemcpyHostToDevice, h->st));
+    if ((rc = lk_refine(h, h->d_in[0], h->d_in[1], h->p.width, h->d_out, h->g.W, h->st))) return rc;
+    HIPCHK(h, hipMemcpyAsync(disp, h->d_out, npx * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
 }
 
 int sgm_stage_post_filter(sgm_handle *h, float *disp) {

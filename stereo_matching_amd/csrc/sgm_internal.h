@@ -94,6 +94,10 @@ hipError_t launch_cc_merge(const float *F, int *L, Geom g, hipStream_t st);
 hipError_t launch_cc_count(int *L, const int *cnt, int *area, Geom g, hipStream_t st);
 hipError_t launch_cc_apply(float *F, const int *L, const int *area, int max_size, float value,
                            Geom g, hipStream_t st);
+// LKRefine (sgm_lk.hip): left/right full-size images (decimated by g.scale on
+// the fly), din the working-grid map, dout (pitched) the refined map.
+hipError_t launch_lk_refine(const uint8_t *left, const uint8_t *right, int pitch, const float *din,
+                            float *dout, int out_pitch, Geom g, hipStream_t st);
 hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
                      Geom g, hipStream_t st);
 

@@ -35,7 +35,8 @@ class SGM:
 
     def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0,
                  blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
-                 uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False):
+                 uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False,
+                 lk_refine: bool = False):
         self._lib = lib()
         p = _capi.default_params(h, w, s, d)
         p.blur = int(bool(blur))
@@ -43,6 +44,8 @@ class SGM:
         # post_filter: process_device's output is post_filter()ed on the GPU
         # (SGM.cpp:821); process() keeps the LR map and get_disp() filters it
         p.post_filter = int(bool(post_filter))
+        # lk_refine: ... then LKRefine (SGM.cpp:824, commented out in the reference)
+        p.lk_refine = int(bool(lk_refine))
         p.p1, p.p2 = p1, p2
         p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
         self.params = p
@@ -92,7 +95,7 @@ class SGM:
                                     self.cols, _ptr(self._lr), self.cols, _ptr(self._raw)),
               self._h)
         self._final = None
-        if self.params.post_filter:  # sgm_process returned get_disp() itself
+        if self.params.post_filter or self.params.lk_refine:  # sgm_process returned the final map
             self._final, self._lr = self._lr, None
 
     def process_device(self, d_left: int, d_right: int, d_out: int, *, pitch: int | None = None,
@@ -132,6 +135,26 @@ class SGM:
         check(self._lib.sgm_post_filter_device(self._h, ctypes.c_void_p(d_disp),
                                                pitch or self.cols,
                                                ctypes.c_void_p(stream or None)), self._h)
+
+    def lk_refine(self, img_l, img_r, disp) -> np.ndarray:
+        """LKSubPixel::LKRefine(img_l, img_r, disp_float) (LKSubPixelImpl.cpp:
+        13-235) on the GPU: full-size images, working-grid map; returns a
+        refined copy (sgm_stage_lk_refine)."""
+        l = _u8(img_l, (self.h, self.w), "img_l")
+        r = _u8(img_r, (self.h, self.w), "img_r")
+        f = np.array(disp, dtype=np.float32, copy=True, order="C")
+        if f.shape != (self.rows, self.cols):
+            raise ValueError(f"disp: expected shape {(self.rows, self.cols)}, got {f.shape}")
+        check(self._lib.sgm_stage_lk_refine(self._h, _ptr(l), _ptr(r), self.w, _ptr(f)), self._h)
+        return f
+
+    def lk_refine_device(self, d_left: int, d_right: int, d_disp: int, *, pitch: int | None = None,
+                         disp_pitch: int | None = None, stream: int = 0) -> None:
+        """In place on a device map (sgm_lk_refine_device)."""
+        check(self._lib.sgm_lk_refine_device(
+            self._h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), pitch or self.w,
+            ctypes.c_void_p(d_disp), disp_pitch or self.cols, ctypes.c_void_p(stream or None)),
+            self._h)
 
     def get_raw_disp(self) -> np.ndarray:
         """Left WTA disparity (SGM.cpp:411-415), uint16, invalid = D+1."""

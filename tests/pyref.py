@@ -246,3 +246,74 @@ def post_filter(F, D, scale=1):
                 for a, b in comp:
                     F[a, b] = D + 1
     return F
+
+
+def lk_refine(L, R, disp, D):
+    """LKRefineCore (LKRefine/LKSubPixelImpl.cpp:56-235), pure numpy float32
+    scalars, with the fp32 evaluation order pinned in oracle/sgm_oracle.c."""
+    L = np.asarray(L, np.int64)
+    R = np.asarray(R, np.int64)
+    F = np.array(disp, np.float32, copy=True)
+    H, W = F.shape
+    hw = 3
+    Ix = np.zeros((H, W), np.float32)
+    dt = F.copy()
+    nd = F.copy()
+    for i in range(hw, H - hw):
+        for j in range(hw, W - hw):
+            Ix[i, j] = f32(L[i, j + 1] - L[i, j - 1]) * f32(0.5)
+            nd[i, j] = f32(int(F[i, j]))
+            dt[i, j] = f32(int(F[i, j]))
+    wcorner = f32(np.exp(-1.0))
+    for i in range(hw, H - hw):
+        for j in range(hw, W - hw):
+            if not Ix[i, j] > 2:
+                continue
+            d0 = dt[i, j]
+            if not (d0 > 0 and d0 < D):
+                continue
+            last_disp, last_doff, last_diff = d0, f32(0), f32(np.finfo(np.float32).max)
+            for _ in range(10):
+                w, jx, res = [], [], []
+                valid = 0
+                for v in range(-hw, hw + 1):
+                    for u in range(-hw, hw + 1):
+                        m, n = i + v, j + u
+                        dm = dt[m, n]
+                        dw = dm + last_doff
+                        ok = (Ix[m, n] > 2 and dm > 0 and dm < D and abs(d0 - dm) <= 2
+                              and not (f32(n) - dw < 0 or f32(n) - dw > f32(W - 1)))
+                        if not ok:
+                            w.append(f32(0)); jx.append(f32(0)); res.append(f32(0))
+                            continue
+                        w.append(wcorner if v * v + u * u >= 18 else f32(1))
+                        res.append(f32(R[m, int(f32(n) - dw)] - L[m, n]))
+                        jx.append(Ix[m, n])
+                        valid += 1
+                if valid < 4.9:
+                    break
+                s2 = f32(0)
+                for x in w:
+                    s2 = f32(s2 + x * x)
+                nrm = np.sqrt(s2)
+                w = [x / nrm for x in w]
+                hs = f32(0)
+                for a, b in zip(jx, w):
+                    hs = f32(hs + (a * b) * a)
+                if float(hs) < 1e-3:
+                    break
+                hinv = f32(1) / hs
+                doff = f32(0)
+                for a, b, r in zip(jx, w, res):
+                    doff = f32(doff + ((hinv * a) * b) * r)
+                if abs(doff - last_doff) > last_diff:
+                    break
+                if not (d0 + doff > 0 and d0 + doff < D):
+                    break
+                last_disp = d0 + doff
+                last_diff = abs(doff - last_doff)
+                last_doff = doff
+                if float(last_diff) < 1e-6:
+                    break
+            nd[i, j] = last_disp
+    return nd

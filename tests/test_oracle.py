@@ -297,3 +297,36 @@ def test_post_filter_median_fill_is_sequential():
     G[6, 3:6] = D + 1
     out = oracle.post_filter(G.copy(), D)
     assert np.array_equal(out.view(np.uint32), pyref.post_filter(G, D).view(np.uint32))
+
+
+@pytest.mark.parametrize("kind", ["road", "noise"])
+def test_lk_refine_oracle_vs_numpy(kind):
+    # LKRefine (LKSubPixelImpl.cpp:56-235) on the map SGM::process hands it
+    # (post-filtered, SGM.cpp:821-824), C oracle vs the numpy restatement
+    from stereo_matching_amd import synthetic
+    h, w, D = 30, 72, 32
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=1, kind=kind)
+    ref = oracle.process(left, right, D, blur=False)
+    disp = ref["final"]
+    got = oracle.lk_refine(left, right, disp, D)
+    want = pyref.lk_refine(left, right, disp, D)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    inner = np.s_[3:-3, 3:-3]
+    # interior: truncated or refined; border: untouched
+    assert np.array_equal(got[:3].view(np.uint32), disp[:3].view(np.uint32))
+    if kind == "road":
+        assert (got[inner] != np.trunc(disp[inner])).any()
+
+
+def test_lk_refine_known_answer():
+    # A pure shift by 5 on a ramp (Ix = 3 > 2): R(x - 5) = L(x), so every
+    # slot has Ires = 0, doff = 0 after one iteration, and a truncated
+    # disparity of 5 (from 5.7) is the answer.
+    H, W, D = 20, 60, 32
+    L = np.tile((np.arange(W) * 3) % 256, (H, 1)).astype(np.uint8)
+    R = np.zeros_like(L)
+    R[:, :W - 5] = L[:, 5:]
+    disp = np.full((H, W), 5.7, np.float32)
+    got = oracle.lk_refine(L, R, disp, D)
+    assert np.array_equal(got.view(np.uint32), pyref.lk_refine(L, R, disp, D).view(np.uint32))
+    assert np.allclose(got[3:-3, 3:-3][:, 3:W - 15], 5.0)
