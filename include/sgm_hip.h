@@ -69,6 +69,9 @@ typedef struct sgm_params {
                           0 (default): the LR-checked map (filtered_disp at SGM.cpp:818) */
     int lk_refine;     /* 1: then LKRefine on the GPU (LKSubPixelImpl.cpp:13-235; the call
                           at SGM.cpp:824 is commented out in the reference); 0 (default) */
+    int sky_detect;    /* 1: the sky masks of both views come from SkyAreaDetector::detect
+                          run on the GPU over the input images (node.cpp:80-93), replacing
+                          any masks passed in; 0 (default): masks as passed (or none) */
 } sgm_params;
 
 typedef struct sgm_handle sgm_handle;
@@ -137,6 +140,17 @@ int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream
 int sgm_lk_refine_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                          float *d_disp, int disp_pitch, void *stream);
 
+/* SkyAreaDetector::detect(img, file, sky_label, scale) (sky_detector/
+ * imageSkyDetector.cpp:166-208) on the GPU: d_img a DEVICE u8 image at the
+ * handle's full size (height x width, pitch bytes); d_mask the DEVICE u8 mask
+ * on the working grid (rows x cols, mask_pitch bytes), 255 = sky.  Four
+ * launches on `stream` (NULL = the handle's stream), no host round trip.
+ * Numerics pinned as oracle/sgm_oracle.c:orc_sky_detect (which reproduces
+ * the reference's example/000017_14 mask exactly).  The debug image the
+ * reference writes to `file` is not produced. */
+int sgm_sky_detect_device(sgm_handle *h, const uint8_t *d_img, int pitch, uint8_t *d_mask,
+                          int mask_pitch, void *stream);
+
 /* ---- per-kernel timing (HIP events recorded around every launch) ---- */
 
 typedef struct sgm_kernel_stat {
@@ -178,6 +192,9 @@ int sgm_stage_post_filter(sgm_handle *h, float *disp);
  * images (pitch bytes), disp a rows x cols map refined in place; synchronous. */
 int sgm_stage_lk_refine(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
                         float *disp);
+/* Sky detector (sgm_sky_detect_device) with HOST buffers: img full-size
+ * (pitch bytes), mask rows x cols; synchronous. */
+int sgm_stage_sky_detect(sgm_handle *h, const uint8_t *img, int pitch, uint8_t *mask);
 
 #ifdef __cplusplus
 }

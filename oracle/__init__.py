@@ -56,6 +56,7 @@ def lib():
         L.orc_lr_check.argtypes = [P, P, I, I, I, I, F]
         L.orc_post_filter.argtypes = [P, I, I, I, I]
         L.orc_lk_refine.argtypes = [P, P, P, I, I, I]
+        L.orc_sky_detect.argtypes = [P, I, I, I, I, P]
         L.orc_process.argtypes = [P, P, P, P, I, I, I, I, I, I, F, F, I, I, ctypes.POINTER(_Result)]
         L.orc_process.restype = I
         L.orc_max_threads.restype = I
@@ -170,6 +171,16 @@ def lk_refine(left, right, disp, D):
     assert L.shape == R.shape == (H, W)
     lib().orc_lk_refine(_p(L), _p(R), _p(F), H, W, D)
     return F
+
+
+def sky_detect(img, scale=1):
+    """SkyAreaDetector::detect (imageSkyDetector.cpp:166-208): u8 mask on the
+    working grid, 255 = sky."""
+    img = _c(img, np.uint8)
+    h, w = img.shape
+    mask = np.empty((h // scale, w // scale), np.uint8)
+    lib().orc_sky_detect(_p(img), h, w, w, scale, _p(mask))
+    return mask
 
 
 def process(left, right, D, scale=1, sky_l=None, sky_r=None, P1=10, P2=100,

@@ -547,6 +547,145 @@ void orc_lk_refine(const uint8_t *L, const uint8_t *R, float *disp, int H, int W
     free(nd);
 }
 
+/* ---------------------------------------------------------- sky detector */
+
+static int sky_cmp_sobel2(const uint8_t *G, int H, int W, int r, int c)
+{
+    /* cv::Sobel(gray, CV_64F, 1, 0) and (0, 1), ksize 3, BORDER_REFLECT_101:
+     * squared magnitude as an exact integer (imageSkyDetector.cpp:215-232) */
+    const int rm = r > 0 ? r - 1 : (H > 1 ? 1 : 0), rp = r < H - 1 ? r + 1 : (H > 1 ? H - 2 : 0);
+    const int cm = c > 0 ? c - 1 : (W > 1 ? 1 : 0), cp = c < W - 1 ? c + 1 : (W > 1 ? W - 2 : 0);
+#define PX(a, b) ((int)G[(i64)(a) * W + (b)])
+    const int dx = (PX(rm, cp) + 2 * PX(r, cp) + PX(rp, cp)) - (PX(rm, cm) + 2 * PX(r, cm) + PX(rp, cm));
+    const int dy = (PX(rp, cm) + 2 * PX(rp, c) + PX(rp, cp)) - (PX(rm, cm) + 2 * PX(rm, c) + PX(rm, cp));
+#undef PX
+    return dx * dx + dy * dy;
+}
+
+/* SkyAreaDetector::detect (sky_detector/imageSkyDetector.cpp:166-208) on a
+ * single-channel image, the path node.cpp:82-86 uses: extract_sky (:76-88) =
+ * extract_border_optimal (:240-281) + check_sky_border_by_gray_value
+ * (:90-164) + make_sky_mask (:796-829, type 1).  refine_border / kmeans
+ * (:356-557) are not on that path.
+ *
+ * Pinned numerics (OpenCV is not in this image):
+ *  - scale > 1: cv::resize INTER_LINEAR to (w/s, h/s) as the 8U fixed-point
+ *    2x2 average (sum + 2) >> 2 (s = 2, the only legal scale);
+ *  - grad = sqrt(dx^2 + dy^2) > t  <=>  dx^2 + dy^2 > t^2 (integers, t <= 362);
+ *  - the image is gray replicated to BGR (:175), so each 3x3 channel
+ *    covariance is v * ones(3,3): determinant 0, largest eigenvalue 3v, with
+ *    v = (n*S2 - S1^2) / n^2 from exact integer moments;
+ *  - calculate_sky_energy (:564-705) = 1 / ((2*det_s + det_g) + (2*eig_s + eig_g)).
+ * The grad_y probe at :309-314 reads (row +- 1, col +- 1) with the row-major
+ * flat index (col -1 / W wrap into the neighbouring row), as cv::Mat::at
+ * does; it is never reached for row <= 5.
+ * mask: rows x cols, 255 = sky, 0 = not (the sky_label of :180-194). */
+void orc_sky_detect(const uint8_t *img, int h, int w, int pitch, int scale, uint8_t *mask)
+{
+    const int H = h / scale, W = w / scale;
+    const i64 n = (i64)H * W;
+    uint8_t *G = (uint8_t *)malloc((size_t)n);
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            if (scale == 1) {
+                G[(i64)i * W + j] = img[(i64)i * pitch + j];
+            } else {
+                const uint8_t *a = img + (i64)(2 * i) * pitch + 2 * j, *b = a + pitch;
+                G[(i64)i * W + j] = (uint8_t)(((int)a[0] + a[1] + b[0] + b[1] + 2) >> 2);
+            }
+        }
+    /* extract_border_optimal: n = floor((600-5)/5)+1 = 120 thresholds,
+     * step = floor(595/120) - 1 = 3, t_k = 5 + 3(k-1) (:248-263) */
+    const double tmax = 600, tmin = 5, tstep = 5;
+    const int nt = (int)floor((tmax - tmin) / tstep) + 1;
+    const double step = floor((tmax - tmin) / nt) - 1;
+    int *b = (int *)malloc(sizeof(int) * (size_t)W);
+    int *best = (int *)malloc(sizeof(int) * (size_t)W);
+    for (int c = 0; c < W; ++c) best[c] = H - 1;
+    /* totals of the non-zero pixels (calculate_sky_energy skips (0,0,0)) */
+    long long N = 0, S1 = 0, S2 = 0;
+    for (i64 k = 0; k < n; ++k)
+        if (G[k]) { ++N; S1 += G[k]; S2 += (long long)G[k] * G[k]; }
+    double jn_max = 0.0;
+    const int half = H / 2;
+    for (int k = 1; k < nt + 1; ++k) {
+        const double t = tmin + step * (k - 1);
+        const long long t2 = (long long)t * (long long)t;
+        long long ns = 0, s1 = 0, s2 = 0;
+        for (int c = 0; c < W; ++c) {
+            /* extract_border (:288-343) */
+            int row_index = -1, bc = -1;
+            for (int row = 0; row < H; ++row) {
+                row_index = row;
+                if (sky_cmp_sobel2(G, H, W, row, c) > t2) {
+                    if (row <= 5) { bc = -1; break; }   /* overwritten at :340-342 */
+                    const i64 up = (i64)(row - 1) * W + c, dn = (i64)(row + 1) * W + c;
+                    const int gy = (2 * G[dn] + G[dn + 1] + G[dn - 1]) - (2 * G[up] + G[up + 1] + G[up - 1]);
+                    bc = gy > 0 ? -1 : row;
+                    break;
+                }
+                if (row_index >= half) { bc = -1; break; }
+            }
+            if (row_index >= half) bc = -1;
+            if (row_index <= 5) bc = -1;
+            b[c] = bc;
+            for (int row = 0; row < bc; ++row) {   /* sky: row < border (:639) */
+                const int g = G[(i64)row * W + c];
+                if (g) { ++ns; s1 += g; s2 += (long long)g * g; }
+            }
+        }
+        double jn;
+        const long long ng = N - ns, g1 = S1 - s1, g2 = S2 - s2;
+        if (ng == 0 || ns == 0) {
+            jn = DBL_MIN;                             /* :650-652 */
+        } else {
+            const double vs = (double)(ns * s2 - s1 * s1) / ((double)ns * (double)ns);
+            const double vg = (double)(ng * g2 - g1 * g1) / ((double)ng * (double)ng);
+            const int para = 2;
+            const double sky_det = 0.0, ground_det = 0.0;
+            jn = 1 / ((para * sky_det + ground_det) + (para * (3 * vs) + (3 * vg)));
+        }
+        if (jn > jn_max) {                           /* :273-276 */
+            jn_max = jn;
+            memcpy(best, b, sizeof(int) * (size_t)W);
+        }
+    }
+    /* check_sky_border_by_gray_value (:90-164) */
+    for (int i = 0; i < W; ++i) {
+        const int border = best[i];
+        for (int j = 0; j < border; ++j)
+            if (G[(i64)j * W + i] < 128) { best[i] = -1; break; }
+        if (border != -1 && (i > 1 && best[i - 1] == -1) && (i < W - 1 && best[i + 1] == -1))
+            best[i] = -1;
+    }
+    {
+        const double f_thres_sky_width = 30;
+        int p = -1, q = -1;
+        for (int i = 0; i < W; ++i) {
+            if (best[i] != -1) {
+                p = i;
+                if (i == W - 1) q = W;
+                for (int j = i + 1; j < W; ++j) {
+                    if (best[j] == -1 || j == W - 1) {
+                        q = j;
+                        if (j == W - 1) q = W;
+                        break;
+                    }
+                }
+                if (q > p && q - p < f_thres_sky_width)
+                    for (int j = p; j < q; ++j) best[j] = -1;
+                i = q;
+            }
+        }
+    }
+    /* make_sky_mask type 1 (:804-812): row <= border */
+    for (int r = 0; r < H; ++r)
+        for (int c = 0; c < W; ++c) mask[(i64)r * W + c] = r <= best[c] ? 255 : 0;
+    free(G);
+    free(b);
+    free(best);
+}
+
 /* --------------------------------------------------------- whole process */
 
 int orc_process(const uint8_t *left, const uint8_t *right,

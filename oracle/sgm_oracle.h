@@ -84,6 +84,11 @@ void orc_post_filter(float *F, int H, int W, int D, int scale);
  * the pinned fp32 evaluation order of its Eigen expressions. */
 void orc_lk_refine(const uint8_t *L, const uint8_t *R, float *disp, int H, int W, int D);
 
+/* SkyAreaDetector::detect (sky_detector/imageSkyDetector.cpp:166-208) on a
+ * single-channel h x w image (row pitch bytes) at scale s: mask on the
+ * working grid (h/s x w/s), 255 = sky.  Pinned numerics: see sgm_oracle.c. */
+void orc_sky_detect(const uint8_t *img, int h, int w, int pitch, int scale, uint8_t *mask);
+
 typedef struct orc_result {
     /* all optional (NULL = not wanted); sizes use the working (decimated) h, w */
     int32_t *disp;          /* left WTA disparity, HW */

@@ -25,7 +25,8 @@ EXPORTS = (
     "sgm_device_bytes", "sgm_process", "sgm_process_device", "sgm_post_filter_host",
     "sgm_post_filter_device", "sgm_stage_census", "sgm_stage_cost", "sgm_stage_path",
     "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
-    "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine",
+    "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine", "sgm_sky_detect_device",
+    "sgm_stage_sky_detect",
 )
 
 
@@ -41,7 +42,7 @@ class Params(ctypes.Structure):
         ("max_disp", ctypes.c_int), ("p1", ctypes.c_int), ("p2", ctypes.c_int),
         ("uniqueness", ctypes.c_float), ("lr_max_diff", ctypes.c_float),
         ("blur", ctypes.c_int), ("views", ctypes.c_int), ("post_filter", ctypes.c_int),
-        ("lk_refine", ctypes.c_int),
+        ("lk_refine", ctypes.c_int), ("sky_detect", ctypes.c_int),
     ]
 
 
@@ -88,6 +89,8 @@ def lib():
     L.sgm_stage_post_filter.argtypes = [P, P]
     L.sgm_lk_refine_device.argtypes = [P, P, P, I, P, I, P]
     L.sgm_stage_lk_refine.argtypes = [P, P, P, I, P]
+    L.sgm_sky_detect_device.argtypes = [P, P, I, P, I, P]
+    L.sgm_stage_sky_detect.argtypes = [P, P, I, P]
     L.sgm_stage_census.argtypes = [P, P, I, P]
     L.sgm_stage_cost.argtypes = [P, P, P, P, I, I, P]
     L.sgm_stage_path.argtypes = [P, I, P, P, P]

@@ -60,6 +60,7 @@ struct sgm_handle {
     int *h_pf_changes;    // pinned readback of one counter
     int pf_iters;         // median launches of the last post filter
     float *d_lk_in;       // LKRefine input copy (the kernel refines the map in place)
+    uint8_t *d_sky_scratch;  // sky detector scratch (sgm_sky.hip)
     uint8_t *h_pin;       // pinned host staging for sgm_process (allocated on first use)
     size_t h_pin_bytes;
     char err[512];
@@ -145,6 +146,7 @@ void free_all(sgm_handle *h) {
     (void)hipFree(h->d_pf_count); (void)hipFree(h->d_pf_area); (void)hipFree(h->d_pf_snap);
     (void)hipFree(h->d_pf_changes);
     (void)hipFree(h->d_lk_in);
+    (void)hipFree(h->d_sky_scratch);
     if (h->h_pf_changes) (void)hipHostFree(h->h_pf_changes);
     h->h_pf_changes = nullptr;
     (void)hipFree(h->d_min);
@@ -321,6 +323,16 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // second stream.
     hipStream_t aux1 = h->concurrent_views ? h->aux[0] : st;  // right view
     const double npx = (double)g.H * g.W;
+    if (h->p.sky_detect) {  // node.cpp:80-93: detect on both inputs, then process with the masks
+        for (int v = 0; v < h->nviews; ++v)
+            HIPCHK(h, timed(h, "sky_detect", npx, st, [&] {
+                       return sgm::launch_sky_detect(v ? d_right : d_left, pitch, h->d_sky[v], g.W,
+                                                     h->d_sky_scratch, g, st);
+                   }));
+        d_sky_l = h->d_sky[0];
+        d_sky_r = h->nviews == 2 ? h->d_sky[1] : nullptr;
+        sky_pitch = g.W;
+    }
     HIPCHK(h, timed(h, "census", npx, st, [&] {
                return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st);
            }));
@@ -474,6 +486,7 @@ int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
     p->views = 2;            // SGM.cpp:448-818
     p->post_filter = 0;      // out = LR-checked map (SGM.cpp:818); 1: + post_filter (:821)
     p->lk_refine = 0;        // 1: + LKRefine (SGM.cpp:824, commented out in the reference)
+    p->sky_detect = 0;       // 1: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
     return SGM_OK;
 }
 
@@ -549,6 +562,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         if (!rc) rc = dalloc(h, &h->d_pf_area, npx);
         if (!rc) rc = dalloc(h, &h->d_pf_snap, sgm::post_snapshot_floats(h->g));
         if (!rc) rc = dalloc(h, &h->d_lk_in, npx);
+        if (!rc) rc = dalloc(h, &h->d_sky_scratch, sgm::sky_scratch_bytes(h->g));
         if (!rc) rc = dalloc(h, &h->d_pf_changes, (size_t)kMedianMaxLaunches);
         if (!rc && hipHostMalloc((void **)&h->h_pf_changes, sizeof(int), hipHostMallocDefault) !=
                        hipSuccess)
@@ -823,6 +837,33 @@ int sgm_stage_lk_refine(sgm_handle *h, const uint8_t *left, const uint8_t *right
     HIPCHK(h, hipMemcpyAsync(h->d_out, disp, npx * 4, hipMemcpyHostToDevice, h->st));
     if ((rc = lk_refine(h, h->d_in[0], h->d_in[1], h->p.width, h->d_out, h->g.W, h->st))) return rc;
     HIPCHK(h, hipMemcpyAsync(disp, h->d_out, npx * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return SGM_OK;
+}
+
+int sgm_sky_detect_device(sgm_handle *h, const uint8_t *d_img, int pitch, uint8_t *d_mask,
+                          int mask_pitch, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!d_img || !d_mask || pitch < h->p.width || mask_pitch < h->g.W)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_sky_detect_device: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    HIPCHK(h, timed(h, "sky_detect", (double)h->g.H * h->g.W, st, [&] {
+               return sgm::launch_sky_detect(d_img, pitch, d_mask, mask_pitch, h->d_sky_scratch,
+                                             h->g, st);
+           }));
+    return SGM_OK;
+}
+
+int sgm_stage_sky_detect(sgm_handle *h, const uint8_t *img, int pitch, uint8_t *mask) {
+    if (!h || !img || !mask || pitch < h->p.width) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    int rc;
+    if ((rc = copy_in_image(h, h->d_in[0], img, pitch))) return rc;
+    if ((rc = sgm_sky_detect_device(h, h->d_in[0], h->p.width, h->d_sky[0], h->g.W, h->st)))
+        return rc;
+    HIPCHK(h, hipMemcpyAsync(mask, h->d_sky[0], npx, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return SGM_OK;
 }

@@ -98,6 +98,11 @@ hipError_t launch_cc_apply(float *F, const int *L, const int *area, int max_size
 // the fly), din the working-grid map, dout (pitched) the refined map.
 hipError_t launch_lk_refine(const uint8_t *left, const uint8_t *right, int pitch, const float *din,
                             float *dout, int out_pitch, Geom g, hipStream_t st);
+// SkyAreaDetector::detect (sgm_sky.hip): img full-size (decimated by g.scale),
+// mask on the working grid; scratch of sky_scratch_bytes(g) bytes.
+size_t sky_scratch_bytes(Geom g);
+hipError_t launch_sky_detect(const uint8_t *img, int pitch, uint8_t *mask, int mask_pitch,
+                             void *scratch, Geom g, hipStream_t st);
 hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
                      Geom g, hipStream_t st);
 

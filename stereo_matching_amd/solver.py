@@ -36,7 +36,7 @@ class SGM:
     def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0,
                  blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
                  uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False,
-                 lk_refine: bool = False):
+                 lk_refine: bool = False, sky_detect: bool = False):
         self._lib = lib()
         p = _capi.default_params(h, w, s, d)
         p.blur = int(bool(blur))
@@ -46,6 +46,8 @@ class SGM:
         p.post_filter = int(bool(post_filter))
         # lk_refine: ... then LKRefine (SGM.cpp:824, commented out in the reference)
         p.lk_refine = int(bool(lk_refine))
+        # sky_detect: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
+        p.sky_detect = int(bool(sky_detect))
         p.p1, p.p2 = p1, p2
         p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
         self.params = p
@@ -155,6 +157,20 @@ class SGM:
             self._h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), pitch or self.w,
             ctypes.c_void_p(d_disp), disp_pitch or self.cols, ctypes.c_void_p(stream or None)),
             self._h)
+
+    def sky_detect(self, img) -> np.ndarray:
+        """SkyAreaDetector::detect(img, ..., scale) (imageSkyDetector.cpp:166-208)
+        on the GPU: u8 mask on the working grid, 255 = sky."""
+        img = _u8(img, (self.h, self.w), "img")
+        mask = np.empty((self.rows, self.cols), np.uint8)
+        check(self._lib.sgm_stage_sky_detect(self._h, _ptr(img), self.w, _ptr(mask)), self._h)
+        return mask
+
+    def sky_detect_device(self, d_img: int, d_mask: int, *, pitch: int | None = None,
+                          mask_pitch: int | None = None, stream: int = 0) -> None:
+        check(self._lib.sgm_sky_detect_device(self._h, ctypes.c_void_p(d_img), pitch or self.w,
+                                              ctypes.c_void_p(d_mask), mask_pitch or self.cols,
+                                              ctypes.c_void_p(stream or None)), self._h)
 
     def get_raw_disp(self) -> np.ndarray:
         """Left WTA disparity (SGM.cpp:411-415), uint16, invalid = D+1."""

@@ -317,3 +317,70 @@ def lk_refine(L, R, disp, D):
                     break
             nd[i, j] = last_disp
     return nd
+
+
+def sky_detect(img, scale=1):
+    """SkyAreaDetector::detect (sky_detector/imageSkyDetector.cpp:166-208),
+    numpy restatement with the numerics pinned in oracle/sgm_oracle.c."""
+    img = np.asarray(img, np.int64)
+    if scale > 1:
+        h, w = img.shape[0] // 2 * 2, img.shape[1] // 2 * 2
+        G = (img[0:h:2, 0:w:2] + img[0:h:2, 1:w:2] + img[1:h:2, 0:w:2] + img[1:h:2, 1:w:2] + 2) >> 2
+    else:
+        G = img.copy()
+    H, W = G.shape
+    P = np.pad(G, 1, mode="reflect") if H > 1 and W > 1 else np.pad(G, 1, mode="edge")
+    dx = (P[:-2, 2:] + 2 * P[1:-1, 2:] + P[2:, 2:]) - (P[:-2, :-2] + 2 * P[1:-1, :-2] + P[2:, :-2])
+    dy = (P[2:, :-2] + 2 * P[2:, 1:-1] + P[2:, 2:]) - (P[:-2, :-2] + 2 * P[:-2, 1:-1] + P[:-2, 2:])
+    a = dx * dx + dy * dy
+    flat = G.ravel()
+    nz = G != 0
+    N, S1, S2 = int(nz.sum()), int(G[nz].sum()), int((G[nz] ** 2).sum())
+    half = H // 2
+    rows = np.arange(H)[:, None]
+    best = np.full(W, H - 1)
+    jn_max = 0.0
+    for k in range(1, 121):
+        t = 5 + 3 * (k - 1)
+        b = np.full(W, -1)
+        for c in range(W):
+            hit = np.flatnonzero(a[:half + 1, c] > t * t)
+            if hit.size == 0:
+                continue
+            r = int(hit[0])
+            if r >= half or r <= 5:
+                continue
+            up, dn = (r - 1) * W + c, (r + 1) * W + c
+            gy = (2 * flat[dn] + flat[dn + 1] + flat[dn - 1]) - (2 * flat[up] + flat[up + 1] + flat[up - 1])
+            b[c] = -1 if gy > 0 else r
+        sky = (rows < b[None, :]) & nz
+        ns, s1, s2 = int(sky.sum()), int(G[sky].sum()), int((G[sky] ** 2).sum())
+        ng, g1, g2 = N - ns, S1 - s1, S2 - s2
+        if ng == 0 or ns == 0:
+            jn = np.finfo(np.float64).tiny
+        else:
+            vs = float(ns * s2 - s1 * s1) / (float(ns) * float(ns))
+            vg = float(ng * g2 - g1 * g1) / (float(ng) * float(ng))
+            jn = 1 / ((2 * 0.0 + 0.0) + (2 * (3 * vs) + (3 * vg)))
+        if jn > jn_max:
+            jn_max, best = jn, b.copy()
+    for i in range(W):
+        border = best[i]
+        if border > 0 and (G[:border, i] < 128).any():
+            best[i] = -1
+        if border != -1 and (i > 1 and best[i - 1] == -1) and (i < W - 1 and best[i + 1] == -1):
+            best[i] = -1
+    i = 0
+    while i < W:
+        if best[i] != -1:
+            p = i
+            q = W if i == W - 1 else -1
+            for j in range(i + 1, W):
+                if best[j] == -1 or j == W - 1:
+                    q = W if j == W - 1 else j
+                    break
+            if q > p and q - p < 30:
+                best[p:q] = -1
+            i = q
+        i += 1
+    return np.where(rows <= best[None, :], 255, 0).astype(np.uint8)

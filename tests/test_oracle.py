@@ -4,7 +4,9 @@ The reference ships no tests or golden vectors and cannot be built here, so
 the oracle is pinned by (1) an independent numpy restatement (tests/pyref.py),
 (2) hand-derived known answers for each stage, and (3) the committed golden
 fixtures in tests/golden/ (regression vectors produced by
-tests/golden/make_golden.py).  Parity status: "parity unpinned" (DESIGN.md).
+tests/golden/make_golden.py).  Parity status: "parity unpinned" (DESIGN.md),
+except the sky detector, pinned by the reference's own example output
+(tests/golden/sky_000017_14.npz, tests/golden/make_sky_golden.py).
 """
 from __future__ import annotations
 
@@ -237,7 +239,7 @@ def test_oracle_thread_count_invariance():
 def _golden_files():
     if not os.path.isdir(GOLDEN):
         return []
-    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("sky_"))
 
 
 @pytest.mark.parametrize("name", _golden_files())
@@ -330,3 +332,21 @@ def test_lk_refine_known_answer():
     got = oracle.lk_refine(L, R, disp, D)
     assert np.array_equal(got.view(np.uint32), pyref.lk_refine(L, R, disp, D).view(np.uint32))
     assert np.allclose(got[3:-3, 3:-3][:, 3:W - 15], 5.0)
+
+
+def test_sky_detect_reproduces_reference_example():
+    # golden: the reference's own detect() output for example/000017_14
+    # (tests/golden/make_sky_golden.py recovers input and mask from its PNGs)
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "sky_000017_14.npz"))
+    got = oracle.sky_detect(g["image"])
+    assert np.array_equal(got, g["mask"]), int((got != g["mask"]).sum())
+    assert np.array_equal(pyref.sky_detect(g["image"]), g["mask"])
+
+
+@pytest.mark.parametrize("kind", __import__("sky_images").KINDS)
+@pytest.mark.parametrize("hw,scale", [((60, 150), 1), ((47, 93), 1), ((90, 200), 2), ((11, 40), 1)])
+def test_sky_detect_oracle_vs_numpy(kind, hw, scale):
+    import sky_images
+    img = sky_images.make(kind, hw[0], hw[1], seed=2)
+    assert np.array_equal(oracle.sky_detect(img, scale), pyref.sky_detect(img, scale)), kind
