@@ -11,6 +11,7 @@
  *                                s in {1,2}, d in {32,64,128} -- widened to 256)
  *   process(l, r)                SGM.cpp:32-826     (LR-checked, post-filtered)
  *   process(l, r, sky, sky_b)    SGM.cpp:829-834    (masks kept as members)
+ *   BM(h, w, s, d)               BM.cpp:4-97        (filtered-cost WTA, post-filtered)
  *   get_disp()                   Solver.h:36        (CV_32FC1, invalid = d+1)
  *   show_disp(view)              Solver.cpp:55-93   (2h x w BGR, colormap :652-707)
  *
@@ -197,64 +198,69 @@ protected:
 
 typedef std::shared_ptr<Solver> SolverPtr;
 
-// SGM (inc/SGM.h:10-26): 8-path semi-global matching on libsgm_hip.so.
-class SGM : public Solver {
+// Common body of the two solvers: one libsgm_hip.so handle per object, the
+// whole frame (and post_filter) on the GPU.
+class HipSolver : public Solver {
 public:
-    explicit SGM(int h, int w, int s, int d) : Solver(h, w, s, d) {
-        sgm_params p;
-        if (sgm_default_params(&p, h, w, s, d) != SGM_OK) fail("SGM", "sgm_default_params");
-        p.post_filter = 1;  // process() ends with post_filter(), SGM.cpp:821 (on the GPU)
-        const int rc = sgm_create(&p, device(), &handle_);
-        if (rc != SGM_OK) fail("SGM: sgm_create", handle_ ? sgm_last_error(handle_) : "no device");
-    }
-    virtual ~SGM() {
+    virtual ~HipSolver() {
         if (handle_) sgm_destroy(handle_);
     }
+    HipSolver(const HipSolver &) = delete;
+    HipSolver &operator=(const HipSolver &) = delete;
 
-    SGM(const SGM &) = delete;
-    SGM &operator=(const SGM &) = delete;
-
-    // SGM.cpp:32-826: both views, LR check, then post_filter() (:821), all on the GPU
-    virtual void process(Mat &img_l, Mat &img_r) {
-        if (img_l.rows != img_r.rows || img_l.cols != img_r.cols || img_l.type() != img_r.type() ||
-            img_l.type() != CV_8UC1 || img_l.rows != in_h_ || img_l.cols != in_w_)
-            fail("SGM::process", "inputs must be CV_8UC1 of the constructed size (SGM.cpp:34-38)");
-        this->img_l = img_l;  // shallow, as SGM.cpp:59-60 (decimated on the device)
-        this->img_r = img_r;
-        const bool sky = !sky_mask.empty() && !sky_mask_beta.empty();
-        if (sky && (sky_mask.rows != img_h || sky_mask.cols != img_w ||
-                    sky_mask_beta.rows != img_h || sky_mask_beta.cols != img_w))
-            fail("SGM::process", "sky masks must be CV_8UC1 on the working grid");
-        const int rc = sgm_process(handle_, img_l.data, img_r.data, (int)img_l.step,
-                                   sky ? sky_mask.data : nullptr,
-                                   sky ? sky_mask_beta.data : nullptr,
-                                   sky ? (int)sky_mask.step : 0,
-                                   filtered_disp.template ptr<float>(0),
-                                   (int)(filtered_disp.step / sizeof(float)), nullptr);
-        if (rc != SGM_OK) fail("SGM::process", sgm_last_error(handle_));
-        if (scale > 1) decimate_left();
-    }
-    // SGM.cpp:829-834
+    // SGM.cpp:829-834 / BM.cpp:91-96
     virtual void process(Mat &img_l, Mat &img_r, Mat &sky_mask, Mat &sky_mask_beta) {
         this->sky_mask = sky_mask;
         this->sky_mask_beta = sky_mask_beta;
         process(img_l, img_r);
     }
+    virtual void process(Mat &img_l, Mat &img_r) {
+        if (img_l.rows != img_r.rows || img_l.cols != img_r.cols || img_l.type() != img_r.type() ||
+            img_l.type() != CV_8UC1 || img_l.rows != in_h_ || img_l.cols != in_w_)
+            fail("process", "inputs must be CV_8UC1 of the constructed size (SGM.cpp:34-38)");
+        this->img_l = img_l;  // shallow, as SGM.cpp:59-60 (decimated on the device)
+        this->img_r = img_r;
+        const bool sky = !sky_mask.empty() && (bm_ || !sky_mask_beta.empty());
+        if (sky && (sky_mask.rows != img_h || sky_mask.cols != img_w ||
+                    (!bm_ && (sky_mask_beta.rows != img_h || sky_mask_beta.cols != img_w))))
+            fail("process", "sky masks must be CV_8UC1 on the working grid");
+        const int rc = sgm_process(handle_, img_l.data, img_r.data, (int)img_l.step,
+                                   sky ? sky_mask.data : nullptr,
+                                   sky && !bm_ ? sky_mask_beta.data : nullptr,
+                                   sky ? (int)sky_mask.step : 0,
+                                   filtered_disp.template ptr<float>(0),
+                                   (int)(filtered_disp.step / sizeof(float)), nullptr);
+        if (rc != SGM_OK) fail("process", sgm_last_error(handle_));
+        if (scale > 1) decimate_left();
+    }
 
     sgm_handle *handle() const { return handle_; }
 
+protected:
+    HipSolver(int h, int w, int s, int d, int solver) : Solver(h, w, s, d), bm_(solver == SGM_SOLVER_BM) {
+        sgm_params p;
+        if (sgm_default_params(&p, h, w, s, d) != SGM_OK) fail("Solver", "sgm_default_params");
+        p.solver = solver;
+        p.post_filter = 1;  // process() ends with post_filter(): SGM.cpp:821, BM.cpp:88 (on the GPU)
+        if (bm_) p.views = 1;
+        const int rc = sgm_create(&p, device(), &handle_);
+        if (rc != SGM_OK) fail("sgm_create", handle_ ? sgm_last_error(handle_) : "no device");
+    }
+
 private:
     sgm_handle *handle_ = nullptr;
+    bool bm_;
 
     static int device() {
         const char *e = std::getenv("SGM_AMD_DEVICE");
         return e ? std::atoi(e) : 0;
     }
-    // keep img_l on the working grid for show_disp (SGM.cpp:40-56)
+    // keep img_l on the working grid for show_disp: SGM.cpp:40-56 takes rows
+    // i*scale, BM.cpp:20-31 rows i (both every scale-th column)
     void decimate_left() {
         Mat small(img_h, img_w, CV_8UC1);
         for (int i = 0; i < img_h; ++i) {
-            const unsigned char *src = img_l.template ptr<unsigned char>(i * scale);
+            const unsigned char *src = img_l.template ptr<unsigned char>(bm_ ? i : i * scale);
             unsigned char *dst = small.template ptr<unsigned char>(i);
             for (int j = 0; j < img_w; ++j) dst[j] = src[j * scale];
         }
@@ -262,6 +268,26 @@ private:
     }
 };
 
+// SGM (inc/SGM.h:10-26): 8-path semi-global matching, both views, LR check,
+// post_filter (SGM.cpp:32-826).
+class SGM : public HipSolver {
+public:
+    explicit SGM(int h, int w, int s, int d) : HipSolver(h, w, s, d, SGM_SOLVER_SGM) {}
+    SGM(const SGM &) = delete;
+    SGM &operator=(const SGM &) = delete;
+};
+
+// BM (inc/BM.h:6-19): census cost, the two cost filters and a WTA on the
+// filtered cost (BM.cpp:9-97).  get_disp() is the post-filtered integer
+// disparity (the reference's BM::process never writes filtered_disp).
+class BM : public HipSolver {
+public:
+    explicit BM(int h, int w, int s, int d) : HipSolver(h, w, s, d, SGM_SOLVER_BM) {}
+    BM(const BM &) = delete;
+    BM &operator=(const BM &) = delete;
+};
+
+typedef std::shared_ptr<BM> BMSolverPtr;
 typedef std::shared_ptr<SGM> SGMSolverPtr;
 
 }  // namespace sgm_amd

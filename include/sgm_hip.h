@@ -53,6 +53,12 @@ enum {
     SGM_DIR_L8 = 7  /* right-down -> left-top  */
 };
 
+/* Matching algorithm: the Solver subclasses of the reference (node.cpp:49-50). */
+enum {
+    SGM_SOLVER_SGM = 0,  /* class SGM (inc/SGM.h:10-26, src/SGM.cpp) */
+    SGM_SOLVER_BM = 1    /* class BM (inc/BM.h:6-19, src/BM.cpp): filtered-cost WTA, left view */
+};
+
 typedef struct sgm_params {
     int height;        /* input image rows (before decimation)      Solver(h,..) */
     int width;         /* input image cols                           Solver(.,w,..) */
@@ -72,6 +78,10 @@ typedef struct sgm_params {
     int sky_detect;    /* 1: the sky masks of both views come from SkyAreaDetector::detect
                           run on the GPU over the input images (node.cpp:80-93), replacing
                           any masks passed in; 0 (default): masks as passed (or none) */
+    int solver;        /* SGM_SOLVER_SGM (default) or SGM_SOLVER_BM.  BM: out = the raw
+                          WTA disparity as float (BM.cpp:53-85; post_filter()ed when
+                          post_filter is set, BM.cpp:88), raw_disp = the same as u16;
+                          views, lk_refine and the right sky mask are unused */
 } sgm_params;
 
 typedef struct sgm_handle sgm_handle;

@@ -57,6 +57,8 @@ def lib():
         L.orc_post_filter.argtypes = [P, I, I, I, I]
         L.orc_lk_refine.argtypes = [P, P, P, I, I, I]
         L.orc_sky_detect.argtypes = [P, I, I, I, I, P]
+        L.orc_bm_process.argtypes = [P, P, P, I, I, I, I, F, I, P]
+        L.orc_bm_process.restype = I
         L.orc_process.argtypes = [P, P, P, P, I, I, I, I, I, I, F, F, I, I, ctypes.POINTER(_Result)]
         L.orc_process.restype = I
         L.orc_max_threads.restype = I
@@ -181,6 +183,19 @@ def sky_detect(img, scale=1):
     mask = np.empty((h // scale, w // scale), np.uint8)
     lib().orc_sky_detect(_p(img), h, w, w, scale, _p(mask))
     return mask
+
+
+def bm_process(left, right, D, scale=1, sky=None, uniq=0.7, blur=True):
+    """BM::process (src/BM.cpp:9-97): raw WTA disparity (int32, invalid D+1)."""
+    left = _c(left, np.uint8)
+    right = _c(right, np.uint8)
+    h, w = left.shape
+    sky = None if sky is None else _c(sky, np.uint8)
+    disp = np.empty((h // scale, w // scale), np.int32)
+    rc = lib().orc_bm_process(_p(left), _p(right), _p(sky), h, w, scale, D, uniq, int(bool(blur)),
+                              _p(disp))
+    assert rc == 0
+    return disp
 
 
 def process(left, right, D, scale=1, sky_l=None, sky_r=None, P1=10, P2=100,

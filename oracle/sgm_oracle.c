@@ -686,6 +686,64 @@ void orc_sky_detect(const uint8_t *img, int h, int w, int pitch, int scale, uint
     free(best);
 }
 
+/* ------------------------------------------------------------------ BM */
+
+/* BM::process (src/BM.cpp:9-97): decimation with the rows NOT strided
+ * (:24-25 read img.ptr(i), column j*scale; SGM.cpp:47-48 reads ptr(i*scale)),
+ * build_cost_table + build_dsi_from_table (view 0, sky mask, :39-41), the two
+ * cost filters (:45-46), then a WTA straight on the filtered cost with the
+ * uniqueness test |min_d - sec_min_d| > 2 (:53-85).  disp is int32 (the
+ * reference's uchar, widened), invalid = D+1.  The reference's get_disp()
+ * after BM::process returns post_filter() of a filtered_disp BM never writes
+ * (:88, Solver.cpp:20); see DESIGN.md for what this build returns instead. */
+int orc_bm_process(const uint8_t *left, const uint8_t *right, const uint8_t *sky,
+                   int h, int w, int scale, int D, float uniq, int blur, int32_t *disp)
+{
+    if (h <= 0 || w <= 0 || (scale != 1 && scale != 2) || D <= 0) return -1;
+    const int H = h / scale, W = w / scale;
+    const i64 npx = (i64)H * W;
+    if (W < 5 || H < 3) return -1;
+    uint8_t *l = (uint8_t *)malloc((size_t)npx), *r = (uint8_t *)malloc((size_t)npx);
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            l[(i64)i * W + j] = left[(i64)i * w + (i64)j * scale];
+            r[(i64)i * W + j] = right[(i64)i * w + (i64)j * scale];
+        }
+    uint8_t *lb = l, *rb = r;
+    if (blur) {
+        lb = (uint8_t *)malloc((size_t)npx);
+        rb = (uint8_t *)malloc((size_t)npx);
+        orc_blur(l, lb, H, W);
+        orc_blur(r, rb, H, W);
+    }
+    uint64_t *ctl = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)npx);
+    uint64_t *ctr = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)npx);
+    orc_census(lb, ctl, H, W, scale);
+    orc_census(rb, ctr, H, W, scale);
+    float *cost = (float *)malloc(sizeof(float) * (size_t)(npx * D));
+    orc_dsi(ctl, ctr, sky, cost, H, W, D, scale, 0);
+    orc_hfilter(cost, H, W, D, 5 / scale);
+    orc_vfilter(cost, H, W, D, 3 / scale);
+    const int invalid = D + 1;
+    int sec_min_d = invalid;   /* declared once outside the pixel loops (:54) */
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            const float *c = cost + ((i64)i * W + j) * D;
+            float min_cost = FLT_MAX, sec_min_cost = FLT_MAX;
+            int min_d = invalid;
+            for (int d = 0; d < D; ++d)
+                if (c[d] < min_cost) { min_cost = c[d]; min_d = d; }
+            for (int d = 0; d < D; ++d)
+                if (c[d] < sec_min_cost && c[d] != min_cost) { sec_min_cost = c[d]; sec_min_d = d; }
+            disp[(i64)i * W + j] =
+                (min_cost / sec_min_cost > uniq && abs(min_d - sec_min_d) > 2) ? invalid : min_d;
+        }
+    free(cost); free(ctl); free(ctr);
+    if (blur) { free(lb); free(rb); }
+    free(l); free(r);
+    return 0;
+}
+
 /* --------------------------------------------------------- whole process */
 
 int orc_process(const uint8_t *left, const uint8_t *right,

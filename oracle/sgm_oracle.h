@@ -89,6 +89,11 @@ void orc_lk_refine(const uint8_t *L, const uint8_t *R, float *disp, int H, int W
  * working grid (h/s x w/s), 255 = sky.  Pinned numerics: see sgm_oracle.c. */
 void orc_sky_detect(const uint8_t *img, int h, int w, int pitch, int scale, uint8_t *mask);
 
+/* BM::process (src/BM.cpp:9-97) on full-size inputs: raw WTA disparity of
+ * the filtered cost, int32 rows x cols, invalid = D+1. */
+int orc_bm_process(const uint8_t *left, const uint8_t *right, const uint8_t *sky,
+                   int h, int w, int scale, int D, float uniq, int blur, int32_t *disp);
+
 typedef struct orc_result {
     /* all optional (NULL = not wanted); sizes use the working (decimated) h, w */
     int32_t *disp;          /* left WTA disparity, HW */

@@ -18,6 +18,8 @@ SGM_ERR_INVALID_ARG = 1
 SGM_ERR_OUT_OF_MEMORY = 2
 SGM_ERR_HIP = 3
 SGM_ERR_NO_DEVICE = 4
+SGM_SOLVER_SGM = 0
+SGM_SOLVER_BM = 1
 
 # Every symbol include/sgm_hip.h declares.
 EXPORTS = (
@@ -43,6 +45,7 @@ class Params(ctypes.Structure):
         ("uniqueness", ctypes.c_float), ("lr_max_diff", ctypes.c_float),
         ("blur", ctypes.c_int), ("views", ctypes.c_int), ("post_filter", ctypes.c_int),
         ("lk_refine", ctypes.c_int), ("sky_detect", ctypes.c_int),
+        ("solver", ctypes.c_int),
     ]
 
 

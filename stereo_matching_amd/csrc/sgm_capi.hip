@@ -120,6 +120,10 @@ bool valid_params(const sgm_params *p, char *why, size_t n) {
     const int H = p->height / p->scale, W = p->width / p->scale;
     if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
     if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
+    if (p->solver != SGM_SOLVER_SGM && p->solver != SGM_SOLVER_BM) {
+        snprintf(why, n, "solver must be SGM_SOLVER_SGM or SGM_SOLVER_BM");
+        return false;
+    }
     // the path DP's start handling relies on non-negative penalties (SGM.cpp:27-28 uses 10, 100)
     if (p->p1 < 0 || p->p2 < 0) { snprintf(why, n, "p1 and p2 must be >= 0"); return false; }
     if ((size_t)H * W > (size_t)0x7fffffff) { snprintf(why, n, "image too large"); return false; }
@@ -311,6 +315,41 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st);
 int lk_refine(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
               float *d_map, int map_pitch, hipStream_t st);
 
+// BM::process (src/BM.cpp:9-97): census with BM's row decimation, the left
+// DSI + both cost filters (the vertical filter's fused L3 checkpoints are
+// simply not used), the filtered-cost WTA, then post_filter (:88).
+int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+             const uint8_t *d_sky_l, int sky_pitch, float *d_out, int out_pitch, uint16_t *d_raw,
+             hipStream_t st) {
+    const Geom g = h->g;
+    const double npx = (double)g.H * g.W, elems = npx * g.D;
+    if (h->p.sky_detect) {
+        HIPCHK(h, timed(h, "sky_detect", npx, st, [&] {
+                   return sgm::launch_sky_detect(d_left, pitch, h->d_sky[0], g.W, h->d_sky_scratch,
+                                                 g, st);
+               }));
+        d_sky_l = h->d_sky[0];
+        sky_pitch = g.W;
+    }
+    HIPCHK(h, timed(h, "census", npx, st, [&] {
+               return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st, true);
+           }));
+    HIPCHK(h, timed(h, "census", npx, st, [&] {
+               return sgm::launch_census(d_right, pitch, g, h->p.blur, h->d_ct[1], st, true);
+           }));
+    int rc;
+    if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
+    HIPCHK(h, timed(h, "bm_wta", elems, st, [&] {
+               return sgm::launch_bm_wta(h->d_c[0], h->p.uniqueness, h->d_disp[0], d_out, out_pitch,
+                                         g, st);
+           }));
+    if (d_raw)
+        HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
+                                 hipMemcpyDeviceToDevice, st));
+    if (h->p.post_filter) return post_filter(h, d_out, out_pitch, st);
+    return SGM_OK;
+}
+
 int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
               const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch, float *d_out,
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
@@ -321,6 +360,8 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // Cache through its six readers, which concurrent views would thrash
     // (1.589 vs 1.627 ms per K128 pair).  SGM_CONCURRENT_VIEWS=1 restores the
     // second stream.
+    if (h->p.solver == SGM_SOLVER_BM)
+        return bm_frame(h, d_left, d_right, pitch, d_sky_l, sky_pitch, d_out, out_pitch, d_raw, st);
     hipStream_t aux1 = h->concurrent_views ? h->aux[0] : st;  // right view
     const double npx = (double)g.H * g.W;
     if (h->p.sky_detect) {  // node.cpp:80-93: detect on both inputs, then process with the masks
@@ -487,6 +528,7 @@ int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
     p->post_filter = 0;      // out = LR-checked map (SGM.cpp:818); 1: + post_filter (:821)
     p->lk_refine = 0;        // 1: + LKRefine (SGM.cpp:824, commented out in the reference)
     p->sky_detect = 0;       // 1: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
+    p->solver = SGM_SOLVER_SGM;
     return SGM_OK;
 }
 

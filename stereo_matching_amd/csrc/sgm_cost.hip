@@ -30,7 +30,9 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i >= n ? 2 * n - 2 - i : i;
 }
 
-__device__ __forceinline__ int blur_at(const uint8_t *src, int pitch, int step, int H, int W,
+// rpitch: bytes between working-grid rows (step * pitch for SGM.cpp:47-48's
+// decimation, pitch for BM.cpp:24-25's); step: pixels between columns.
+__device__ __forceinline__ int blur_at(const uint8_t *src, int rpitch, int step, int H, int W,
                                        int y, int x) {
     const int xm = reflect101(x - 1, W) * step, x0 = x * step, xp = reflect101(x + 1, W) * step;
     const int ys[3] = {reflect101(y - 1, H), y, reflect101(y + 1, H)};
@@ -38,7 +40,7 @@ __device__ __forceinline__ int blur_at(const uint8_t *src, int pitch, int step, 
     int acc = 0;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const uint8_t *row = src + (size_t)ys[r] * step * pitch;
+        const uint8_t *row = src + (size_t)ys[r] * rpitch;
         acc += ky[r] * (82 * row[xm] + 93 * row[x0] + 82 * row[xp]);
     }
     const int v = (acc + (1 << 15)) >> 16;
@@ -51,7 +53,7 @@ constexpr int CT_TW = 64, CT_TH = 8;
 // centre skipped, coordinates clamped to the (working-grid) edge.  The
 // (blurred) window is staged in LDS at clamped coordinates.
 template <int HH, int HWW>
-__global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__ src, int pitch,
+__global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__ src, int rpitch,
                                                      int step, int H, int W, int blur,
                                                      uint64_t *__restrict__ ct) {
     constexpr int TR = CT_TH + 2 * HH, TC = CT_TW + 2 * HWW;
@@ -60,8 +62,8 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
     for (int idx = tid_x(); idx < TR * TC; idx += 256) {
         const int ty = idx / TC, tx = idx - ty * TC;
         const int y = clampi(y0 + ty - HH, 0, H - 1), x = clampi(x0 + tx - HWW, 0, W - 1);
-        tile[ty][tx] = blur ? (uint8_t)blur_at(src, pitch, step, H, W, y, x)
-                            : src[(size_t)y * step * pitch + (size_t)x * step];
+        tile[ty][tx] = blur ? (uint8_t)blur_at(src, rpitch, step, H, W, y, x)
+                            : src[(size_t)y * rpitch + (size_t)x * step];
     }
     __syncthreads();
     const int tx = tid_x() & 63;
@@ -82,12 +84,13 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
 }
 
 hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64_t *ct,
-                         hipStream_t st) {
+                         hipStream_t st, bool bm_rows) {
     dim3 grid((g.W + CT_TW - 1) / CT_TW, (g.H + CT_TH - 1) / CT_TH);
+    const int rpitch = bm_rows ? pitch : pitch * g.scale;
     if (g.scale == 1)
-        census_kernel<3, 4><<<grid, 256, 0, st>>>(src, pitch, 1, g.H, g.W, blur, ct);
+        census_kernel<3, 4><<<grid, 256, 0, st>>>(src, rpitch, 1, g.H, g.W, blur, ct);
     else
-        census_kernel<1, 2><<<grid, 256, 0, st>>>(src, pitch, 2, g.H, g.W, blur, ct);
+        census_kernel<1, 2><<<grid, 256, 0, st>>>(src, rpitch, 2, g.H, g.W, blur, ct);
     return hipGetLastError();
 }
 

@@ -36,7 +36,8 @@ class SGM:
     def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0,
                  blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
                  uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False,
-                 lk_refine: bool = False, sky_detect: bool = False):
+                 lk_refine: bool = False, sky_detect: bool = False,
+                 _solver: int = _capi.SGM_SOLVER_SGM):
         self._lib = lib()
         p = _capi.default_params(h, w, s, d)
         p.blur = int(bool(blur))
@@ -48,6 +49,7 @@ class SGM:
         p.lk_refine = int(bool(lk_refine))
         # sky_detect: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
         p.sky_detect = int(bool(sky_detect))
+        p.solver = _solver
         p.p1, p.p2 = p1, p2
         p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
         self.params = p
@@ -225,3 +227,17 @@ class SGM:
         out = np.empty_like(fl)
         check(self._lib.sgm_stage_lr(self._h, _ptr(fl), _ptr(fr), _ptr(out)), self._h)
         return out
+
+
+class BM(SGM):
+    """Block matcher on one MI355X: mirrors ``BM(int h, int w, int s, int d)``
+    (inc/BM.h:6-19, src/BM.cpp:4-97): census cost + the two cost filters and a
+    winner-take-all on the filtered cost (uniqueness |d1 - d2| > 2), then
+    post_filter().  get_disp() is the post-filtered integer disparity (the
+    reference's BM never writes filtered_disp); get_raw_disp() the
+    WTA result."""
+
+    def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0,
+                 blur: bool = True, uniqueness: float = 0.7, sky_detect: bool = False):
+        super().__init__(h, w, s, d, device=device, blur=blur, views=1, uniqueness=uniqueness,
+                         post_filter=True, sky_detect=sky_detect, _solver=_capi.SGM_SOLVER_BM)

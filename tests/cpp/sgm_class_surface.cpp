@@ -3,6 +3,7 @@
 // a pair, read get_disp().
 //   sgm_class_surface nodevice            -> argument asserts + no-device error
 //   sgm_class_surface run L R H W D OUT   -> raw u8 pair in, f32 disparity out
+//   sgm_class_surface runbm L R H W D OUT -> the same through BM(h, w, s, d)
 #define SGM_AMD_THROW 1
 #include "sgm_amd/SGM.h"
 
@@ -37,14 +38,18 @@ int main(int argc, char **argv) {
         bad += m.clone().data == m.data;
         return bad;
     }
-    if (argc == 8 && std::string(argv[1]) == "run") {
+    if (argc == 8 && (std::string(argv[1]) == "run" || std::string(argv[1]) == "runbm")) {
         const int h = std::atoi(argv[4]), w = std::atoi(argv[5]), d = std::atoi(argv[6]);
         Mat l(h, w, CV_8UC1), r(h, w, CV_8UC1);
         std::ifstream fl(argv[2], std::ios::binary), fr(argv[3], std::ios::binary);
         fl.read(reinterpret_cast<char *>(l.data), (std::streamsize)h * w);
         fr.read(reinterpret_cast<char *>(r.data), (std::streamsize)h * w);
         if (!fl || !fr) return 2;
-        sgm_amd::SGMSolverPtr sgm = std::make_shared<sgm_amd::SGM>(h, w, 1, d);
+        sgm_amd::SolverPtr sgm;
+        if (std::string(argv[1]) == "runbm")
+            sgm = std::make_shared<sgm_amd::BM>(h, w, 1, d);
+        else
+            sgm = std::make_shared<sgm_amd::SGM>(h, w, 1, d);
         sgm->process(l, r);
         const Mat &disp = sgm->get_disp();
         Mat view;
@@ -55,6 +60,6 @@ int main(int argc, char **argv) {
             fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
         return fo ? 0 : 4;
     }
-    std::fprintf(stderr, "usage: %s nodevice | run L R H W D OUT\n", argv[0]);
+    std::fprintf(stderr, "usage: %s nodevice | run|runbm L R H W D OUT\n", argv[0]);
     return 2;
 }

@@ -384,3 +384,32 @@ def sky_detect(img, scale=1):
             i = q
         i += 1
     return np.where(rows <= best[None, :], 255, 0).astype(np.uint8)
+
+
+def bm_process(left, right, D, scale=1, sky=None, uniq=0.7, blur_on=True):
+    """BM::process (src/BM.cpp:9-97): rows not strided by the scale (:24-25),
+    cost + filters, WTA with |min_d - sec_min_d| > 2."""
+    left = np.asarray(left, np.uint8)
+    right = np.asarray(right, np.uint8)
+    h, w = left.shape
+    H, W = h // scale, w // scale
+    L = left[:H, 0:W * scale:scale][:, :W]
+    R = right[:H, 0:W * scale:scale][:, :W]
+    if blur_on:
+        L, R = blur(L), blur(R)
+    C = dsi(census(L, scale), census(R, scale), D, scale, 0, sky)
+    C = vfilter(hfilter(C, 5 // scale), 3 // scale)
+    disp = np.empty((H, W), np.int32)
+    for i in range(H):
+        for j in range(W):
+            c = C[i, j]
+            m = c.min()
+            d = int(np.argmax(c == m))
+            rest = c[c != m]
+            if rest.size:
+                s = rest.min()
+                sd = int(np.argmax(c == s))
+                if m / s > f32(uniq) and abs(d - sd) > 2:
+                    d = D + 1
+            disp[i, j] = d
+    return disp

@@ -60,3 +60,21 @@ def test_class_surface_matches_oracle(exe, tmp_path):
     got = np.fromfile(fo, dtype=np.float32).reshape(h, w)
     want = oracle.process(left, right, D, views=2)["final"]
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_bm_class_surface_matches_oracle(exe, tmp_path):
+    # BM(h, w, s, d) through the same Solver pointer the node holds (node.cpp:49-50)
+    import oracle
+    oracle.build()
+    h, w, D = 80, 240, 64
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=4)
+    fl, fr, fo = (str(tmp_path / n) for n in ("l.raw", "r.raw", "out.raw"))
+    left.tofile(fl)
+    right.tofile(fr)
+    r = subprocess.run([exe, "runbm", fl, fr, str(h), str(w), str(D), fo],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(fo, dtype=np.float32).reshape(h, w)
+    want = oracle.post_filter(oracle.bm_process(left, right, D).astype(np.float32), D)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
