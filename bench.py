@@ -44,6 +44,14 @@ CONFIGS = {
                   workload="config3: 1920x1080 D=256, 8-path SGM + LR check (V=2), 1 pair per GPU"),
     "4k256": dict(h=2160, w=3840, D=256, views=2,
                   workload="3840x2160 D=256, 8-path SGM + LR check (V=2), 1 pair per GPU"),
+    # BASELINE.json configs[4] on one GPU: the full pipeline of node.cpp:80-107
+    "4k256full": dict(h=2160, w=3840, D=256, views=2, full=True,
+                      workload="config5: 3840x2160 D=256 full pipeline: sky detector on both "
+                               "views + 8-path SGM + LR check + post_filter + LKRefine (V=2), "
+                               "1 pair per GPU"),
+    "k128full": dict(h=375, w=1242, D=128, views=2, full=True,
+                     workload="KITTI 1242x375 D=128 full pipeline: sky detector on both views + "
+                              "8-path SGM + LR check + post_filter + LKRefine (V=2), 1 pair per GPU"),
 }
 
 # Algorithmic HBM bytes per pixel-disparity element per launch (DESIGN.md
@@ -78,10 +86,14 @@ BYTES_PER_PIXEL = {"census": 9, "lr": 12,
                    "post_median": 8, "post_cc_local": 12, "post_cc_apply": 16,
                    "post_cc_count": 4, "post_cc_merge": 0,
                    # LKRefine: map in + out, 7x7 window and images through LDS/L2
-                   "lk_refine": 10}
+                   "lk_refine": 10,
+                   # sky detector: image in, gray out/in, mask out (+ per-threshold columns)
+                   "sky_detect": 4, "bm_wta": 0}
 
 
 def algorithmic_bytes(name: str, elems: float, D: int) -> float:
+    if name == "bm_wta":
+        return 4.0 * elems  # read the filtered cost once (elems = W*H*D)
     if name in BYTES_PER_PIXEL:
         # per-pixel classes report elems = pixels (census: W*H; post_*: W*H)
         return BYTES_PER_PIXEL[name] * elems
@@ -102,6 +114,8 @@ def parse():
                     help="end each step with post_filter() on the GPU (SGM.cpp:821; V=2 configs)")
     ap.add_argument("--lk-refine", action="store_true",
                     help="end each step with LKRefine on the GPU (SGM.cpp:824, LKSubPixelImpl.cpp)")
+    ap.add_argument("--sky-detect", action="store_true",
+                    help="start each step with the sky detector on both views (node.cpp:80-93)")
     ap.add_argument("--host-io", action="store_true",
                     help="also time sgm_process on host buffers (PCIe-inclusive, not `value`)")
     return ap.parse_args()
@@ -134,8 +148,10 @@ def main():
     d_out = torch.empty((h, w), dtype=torch.float32, device=dev)
     gather = [torch.empty_like(d_out) for _ in range(world)] if (world > 1 and rank == 0) else None
 
+    if cfg.get("full"):
+        args.post_filter = args.lk_refine = args.sky_detect = True
     sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter,
-              lk_refine=args.lk_refine)
+              lk_refine=args.lk_refine, sky_detect=args.sky_detect)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -239,17 +255,29 @@ def main():
         oracle.build()
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         oracle.set_threads(threads)
+        # bounded sample (~0.6 G pixel-disparity units per frame): a band of the
+        # frame's top rows at full width when the frame is larger than that
+        sh = h if views * h * w * D <= 6e8 else max(16, int(6e8 / (views * w * D)))
+        ls, rs = left[:sh], right[:sh]
+        full = bool(cfg.get("full"))
         ts = []
         for _ in range(max(1, args.cpu_frames)):
             t0 = time.perf_counter()
-            oracle.process(left, right, D, views=views)
+            ml = oracle.sky_detect(ls) if full else None
+            mr = oracle.sky_detect(rs) if full else None
+            ref = oracle.process(ls, rs, D, views=views, sky_l=ml, sky_r=mr)
+            if full:
+                oracle.lk_refine(ls, rs, ref["final"], D)
             ts.append(time.perf_counter() - t0)
         tmed = statistics.median(ts)
-        cpu = {"value": round(views * h * w * D / tmed / 1e6, 2), "unit": "Mpixel-disparities/s",
+        what = "full frames" if sh == h else f"bands of the top {sh} rows (full width)"
+        stages = ("sky detector + SGM + LR + post_filter + LKRefine" if full else
+                  "SGM" + (" + LR + post_filter" if views == 2 else ""))
+        cpu = {"value": round(views * sh * w * D / tmed / 1e6, 2), "unit": "Mpixel-disparities/s",
                "cores": oracle.max_threads(), "kind": "port",
-               "sample": f"{len(ts)} full frames of the same workload ({w}x{h} D={D}, V={views}) "
-                         f"through oracle/sgm_oracle.c (C restatement, OpenMP placement of the "
-                         f"reference), median {tmed:.3f} s/frame"}
+               "sample": f"{len(ts)} {what} of the same workload ({w}x{h} D={D}, V={views}; "
+                         f"{stages}) through oracle/sgm_oracle.c (C restatement, OpenMP "
+                         f"placement of the reference), median {tmed:.3f} s per sample"}
 
     if rank == 0:
         rec = {
@@ -257,10 +285,13 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": cfg["workload"] + (" + post_filter" if args.post_filter else "")
+            "config": {"workload": cfg["workload"] if cfg.get("full") else
+                       cfg["workload"] + (" + sky detector" if args.sky_detect else "")
+                       + (" + post_filter" if args.post_filter else "")
                        + (" + LKRefine" if args.lk_refine else ""),
                        "width": w, "height": h, "max_disp": D, "views": views,
-                       "post_filter": bool(args.post_filter), "lk_refine": bool(args.lk_refine), "pairs_per_gpu": 1, "global_batch": world,
+                       "post_filter": bool(args.post_filter), "lk_refine": bool(args.lk_refine),
+                       "sky_detect": bool(args.sky_detect), "pairs_per_gpu": 1, "global_batch": world,
                        "parallelism": f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
             "host_io": host_io,

@@ -7,13 +7,14 @@
 // per-column sky border (first row of the top half whose Sobel magnitude
 // exceeds t_k) that maximises an energy of the sky and ground intensity
 // variances; then drops columns with a dark sky pixel, isolated columns and
-// runs narrower than 30.  Four launches, no host round trip:
+// runs narrower than 30.  Five launches, no host round trip:
 //   1. gray:    working-grid image (2x2 average at scale 2) + moments of all
 //               non-zero pixels;
 //   2. columns: one thread per column scans the top half once: a row whose
 //               |grad|^2 exceeds the next thresholds' t^2 is their border
 //               (or -1), recorded with the sky moments above it; the first
-//               dark (< 128) row; then per-threshold sums over the wave;
+//               dark (< 128) row; then one workgroup per threshold sums the
+//               columns' sky moments;
 //   3. select:  one workgroup: energies, the first maximum, the gray-value
 //               and isolated-column checks (parallel: a dropped isolated
 //               column can never enable its right neighbour's drop), and the
@@ -38,13 +39,18 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
     return v;
 }
 
-// 1. working-grid gray image + totals of the non-zero pixels (tot[kSkyT][*])
+// 1. working-grid gray image + moments of the non-zero pixels: 64 x 16
+// pixels per workgroup, one partial triple per workgroup (summed in 2b).
 __global__ __launch_bounds__(256) void sky_gray_kernel(const uint8_t *__restrict__ img, int pitch,
                                                       int s, uint8_t *__restrict__ G, int H, int W,
-                                                      unsigned long long *tot) {
-    const int j = bid_x() * 64 + (tid_x() & 63), i = bid_y() * 4 + (tid_x() >> 6);
-    long long n = 0, s1 = 0, s2 = 0;
-    if (i < H && j < W) {
+                                                      long long *partial) {
+    __shared__ long long part[3][4];
+    const int lane = tid_x() & 63, wave = tid_x() >> 6;
+    const int j = bid_x() * 64 + lane;
+    int n = 0, s1 = 0, s2 = 0;  // <= 4 pixels per thread
+    for (int r = 0; r < 4; ++r) {
+        const int i = bid_y() * 16 + wave * 4 + r;
+        if (i >= H || j >= W) continue;
         int g;
         if (s == 1) {
             g = img[(size_t)i * pitch + j];
@@ -53,16 +59,14 @@ __global__ __launch_bounds__(256) void sky_gray_kernel(const uint8_t *__restrict
             g = ((int)a[0] + a[1] + b[0] + b[1] + 2) >> 2;
         }
         G[(size_t)i * W + j] = (uint8_t)g;
-        if (g) { n = 1; s1 = g; s2 = (long long)g * g; }
+        if (g) { ++n; s1 += g; s2 += g * g; }
     }
-    n = wave_sum64(n);
-    s1 = wave_sum64(s1);
-    s2 = wave_sum64(s2);
-    if ((tid_x() & 63) == 0 && n) {
-        atomicAdd(tot + 3 * kSkyT + 0, (unsigned long long)n);
-        atomicAdd(tot + 3 * kSkyT + 1, (unsigned long long)s1);
-        atomicAdd(tot + 3 * kSkyT + 2, (unsigned long long)s2);
-    }
+    const long long wn = wave_sum64(n), w1 = wave_sum64(s1), w2 = wave_sum64(s2);
+    if (lane == 0) { part[0][wave] = wn; part[1][wave] = w1; part[2][wave] = w2; }
+    __syncthreads();
+    if (tid_x() < 3)
+        partial[3 * (bid_y() * (int)gridDim.x + bid_x()) + tid_x()] =
+            part[tid_x()][0] + part[tid_x()][1] + part[tid_x()][2] + part[tid_x()][3];
 }
 
 __device__ __forceinline__ int reflect101(int x, int n) {  // BORDER_REFLECT_101
@@ -74,85 +78,134 @@ __device__ __forceinline__ int reflect101(int x, int n) {  // BORDER_REFLECT_101
 
 // 2. per column: the border of every threshold (extract_border, :288-343) with
 // the sky moments above it (calculate_sky_energy, :633-646), the first dark
-// row (check_sky_border_by_gray_value, :101-109); per-threshold wave sums.
-// Rows are read 8 at a time ahead of use (3 pixels each: c-1, c, c+1).
-__global__ __launch_bounds__(64) void sky_columns_kernel(const uint8_t *__restrict__ G, int H,
-                                                        int W, int *__restrict__ B,
-                                                        int *__restrict__ M,
-                                                        int *__restrict__ dark,
-                                                        unsigned long long *tot) {
-    const int c = bid_x() * 64 + tid_x();
+// row (check_sky_border_by_gray_value, :101-109).  A workgroup owns 64
+// columns: its four waves first stage the top-half strip (rows 0..half+1,
+// columns c0-1..c0+64 at reflected coordinates, plus columns W-1 and 0 for the
+// row-wrapping grad_y probe of the edge columns) in LDS, then wave 0 scans it,
+// one lane per column.
+constexpr int kSkyStripW = 68;  // 66 window columns, then G[r][W-1], G[r][0]
+constexpr size_t kSkyStripMax = 160 * 1024 - 1024;
+__global__ __launch_bounds__(256) void sky_columns_kernel(const uint8_t *__restrict__ G, int H,
+                                                         int W, int *__restrict__ B,
+                                                         int *__restrict__ M,
+                                                         int *__restrict__ dark) {
+    extern __shared__ uint8_t strip[];  // [rows 0..last+1][kSkyStripW]
+    const int c0 = bid_x() * 64, t = tid_x();
     const int half = H / 2, last = half < H - 1 ? half : H - 1;
+    const int nrows = last + 2 < H ? last + 2 : H;  // rows 0..last+1 that exist
+    // 8 loads in flight per thread before their LDS stores
+    const int total = nrows * kSkyStripW;
+    for (int q0 = 0; q0 < total; q0 += 8 * 256) {
+        uint8_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * 256 + t;
+            const int r = q / kSkyStripW, x = q - r * kSkyStripW;
+            const int col = x < 66 ? reflect101(c0 - 1 + x, W) : (x == 66 ? W - 1 : 0);
+            v[u] = q < total ? G[(size_t)r * W + col] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * 256 + t;
+            if (q < total) strip[q] = v[u];
+        }
+    }
+    __syncthreads();
+    if (t >= 64) return;
+    const int c = c0 + t;
+    if (c >= W) return;
     const size_t kW = (size_t)kSkyT * W;
-    if (c < W) {
-        const int cm = reflect101(c - 1, W), cp = reflect101(c + 1, W);
-        auto row3 = [&](int r) {  // (G[r][c-1], G[r][c], G[r][c+1]) packed
-            const uint8_t *q = G + (size_t)reflect101(r, H) * W;
-            return (int)q[cm] | ((int)q[c] << 8) | ((int)q[cp] << 16);
-        };
-        int kk = 0, n = 0, s1 = 0, s2 = 0, fd = H;
-        int pv = row3(-1), cu = row3(0);
-        for (int r0 = 0; r0 <= last; r0 += 8) {
-            int nx[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) nx[q] = row3(r0 + q + 1);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int r = r0 + q;
-                if (r > last) break;
-                const int nv = nx[q];
-                // |Sobel|^2, ksize 3 (:215-232)
-                const int dx = (((pv >> 16) & 255) + 2 * ((cu >> 16) & 255) + ((nv >> 16) & 255)) -
-                               ((pv & 255) + 2 * (cu & 255) + (nv & 255));
-                const int dy = ((nv & 255) + 2 * ((nv >> 8) & 255) + ((nv >> 16) & 255)) -
-                               ((pv & 255) + 2 * ((pv >> 8) & 255) + ((pv >> 16) & 255));
-                const long long a = dx * dx + dy * dy;
-                while (kk < kSkyT && a > sky_t2(kk)) {
-                    int b = -1;
-                    if (r < half && r > 5) {
-                        // grad_y (:309-314): row-major flat neighbours, as cv::Mat::at
-                        const size_t up = (size_t)(r - 1) * W + c, dn = (size_t)(r + 1) * W + c;
-                        const int gy = (2 * (int)G[dn] + G[dn + 1] + G[dn - 1]) -
-                                       (2 * (int)G[up] + G[up + 1] + G[up - 1]);
-                        b = gy > 0 ? -1 : r;
-                    }
-                    B[(size_t)kk * W + c] = b;
-                    M[(size_t)kk * W + c] = b < 0 ? 0 : n;
-                    M[kW + (size_t)kk * W + c] = b < 0 ? 0 : s1;
-                    M[2 * kW + (size_t)kk * W + c] = b < 0 ? 0 : s2;
-                    ++kk;
-                }
-                const int g = (cu >> 8) & 255;
-                if (g < 128 && fd == H) fd = r;
-                if (g) { ++n; s1 += g; s2 += g * g; }
-                pv = cu;
-                cu = nv;
-            }
-        }
-        for (; kk < kSkyT; ++kk) {
-            B[(size_t)kk * W + c] = -1;
-            M[(size_t)kk * W + c] = 0;
-            M[kW + (size_t)kk * W + c] = 0;
-            M[2 * kW + (size_t)kk * W + c] = 0;
-        }
-        dark[c] = fd;
-    }
+    auto row3 = [&](int r) {  // (G[r][c-1], G[r][c], G[r][c+1]) packed, reflected
+        const uint8_t *q = strip + reflect101(r, H) * kSkyStripW + t;
+        return (int)q[0] | ((int)q[1] << 8) | ((int)q[2] << 16);
+    };
+    // |Sobel|^2 of row r from rows r-1, r, r+1 (ksize 3, :215-232)
+    auto sob2 = [](int pv, int cu, int nv) {
+        const int dx = (((pv >> 16) & 255) + 2 * ((cu >> 16) & 255) + ((nv >> 16) & 255)) -
+                       ((pv & 255) + 2 * (cu & 255) + (nv & 255));
+        const int dy = ((nv & 255) + 2 * ((nv >> 8) & 255) + ((nv >> 16) & 255)) -
+                       ((pv & 255) + 2 * ((pv >> 8) & 255) + ((pv >> 16) & 255));
+        return (long long)(dx * dx + dy * dy);
+    };
+    // Thresholds in increasing order: the first row whose |grad|^2 > t_k^2
+    // never moves up as k grows, so one pointer walks the column once; the
+    // moments of the rows above it are the sky moments of that border.
+    int r = 0, n = 0, s1 = 0, s2 = 0, fd = H;
+    int pv = row3(-1), cu = row3(0), nv = row3(1);
+    long long a = sob2(pv, cu, nv);
     for (int k = 0; k < kSkyT; ++k) {
-        long long n = 0, s1 = 0, s2 = 0;
-        if (c < W) {
-            n = M[(size_t)k * W + c];
-            s1 = M[kW + (size_t)k * W + c];
-            s2 = (unsigned)M[2 * kW + (size_t)k * W + c];
+        const long long t2 = sky_t2(k);
+        while (r <= last && !(a > t2)) {
+            const int g = (cu >> 8) & 255;
+            if (g < 128 && fd == H) fd = r;
+            if (g) { ++n; s1 += g; s2 += g * g; }
+            ++r;
+            pv = cu;
+            cu = nv;
+            nv = row3(r + 1);
+            a = sob2(pv, cu, nv);
         }
-        n = wave_sum64(n);
-        s1 = wave_sum64(s1);
-        s2 = wave_sum64(s2);
-        if (tid_x() == 0 && n) {
-            atomicAdd(tot + 3 * k + 0, (unsigned long long)n);
-            atomicAdd(tot + 3 * k + 1, (unsigned long long)s1);
-            atomicAdd(tot + 3 * k + 2, (unsigned long long)s2);
+        int b = -1;
+        if (r <= last && r < half && r > 5) {
+            // grad_y (:309-314) reads (r +- 1, c +- 1) by row-major flat index
+            // (cv::Mat::at): the register window for inner columns; at the edge
+            // columns the index wraps into the neighbouring row
+            const uint8_t *sr = strip + t + 1;  // (row 0, column c)
+            auto S = [&](int rr, int dc) { return (int)sr[rr * kSkyStripW + dc]; };
+            int gy;
+            if (c > 0 && c < W - 1) {
+                gy = (2 * ((nv >> 8) & 255) + ((nv >> 16) & 255) + (nv & 255)) -
+                     (2 * ((pv >> 8) & 255) + ((pv >> 16) & 255) + (pv & 255));
+            } else if (c == 0) {  // (r+1, -1) = (r, W-1); (r-1, -1) = (r-2, W-1)
+                gy = (2 * S(r + 1, 0) + S(r + 1, 1) + (int)strip[r * kSkyStripW + 66]) -
+                     (2 * S(r - 1, 0) + S(r - 1, 1) + (int)strip[(r - 2) * kSkyStripW + 66]);
+            } else {              // (r+1, W) = (r+2, 0); (r-1, W) = (r, 0)
+                gy = (2 * S(r + 1, 0) + (int)strip[(r + 2) * kSkyStripW + 67] + S(r + 1, -1)) -
+                     (2 * S(r - 1, 0) + (int)strip[r * kSkyStripW + 67] + S(r - 1, -1));
+            }
+            b = gy > 0 ? -1 : r;
+        }
+        B[(size_t)k * W + c] = b;
+        M[(size_t)k * W + c] = b < 0 ? 0 : n;
+        M[kW + (size_t)k * W + c] = b < 0 ? 0 : s1;
+        M[2 * kW + (size_t)k * W + c] = b < 0 ? 0 : s2;
+    }
+    for (; r <= last && fd == H; ++r)  // the first dark row of the top half
+        if ((int)strip[r * kSkyStripW + t + 1] < 128) fd = r;
+    dark[c] = fd;
+}
+
+// 2b. per threshold k < kSkyT: the sums of the columns' sky moments; block
+// kSkyT: the image totals from the gray kernel's partials
+__global__ __launch_bounds__(256) void sky_reduce_kernel(const int *__restrict__ M, int W,
+                                                        const long long *__restrict__ partial,
+                                                        int npart, unsigned long long *tot) {
+    __shared__ long long part[3][4];
+    const int k = bid_x(), lane = tid_x() & 63, wave = tid_x() >> 6;
+    const size_t kW = (size_t)kSkyT * W;
+    long long n = 0, s1 = 0, s2 = 0;
+    if (k < kSkyT) {
+        const int *m0 = M + (size_t)k * W, *m1 = m0 + kW, *m2 = m1 + kW;
+        for (int c = tid_x(); c < W; c += 256) {
+            n += m0[c];
+            s1 += m1[c];
+            s2 += (unsigned)m2[c];
+        }
+    } else {
+        for (int b = tid_x(); b < npart; b += 256) {
+            n += partial[3 * b];
+            s1 += partial[3 * b + 1];
+            s2 += partial[3 * b + 2];
         }
     }
+    n = wave_sum64(n);
+    s1 = wave_sum64(s1);
+    s2 = wave_sum64(s2);
+    if (lane == 0) { part[0][wave] = n; part[1][wave] = s1; part[2][wave] = s2; }
+    __syncthreads();
+    if (tid_x() < 3)
+        tot[3 * k + tid_x()] = (unsigned long long)(part[tid_x()][0] + part[tid_x()][1] +
+                                                    part[tid_x()][2] + part[tid_x()][3]);
 }
 
 // 3. energies, the chosen border, the column checks (one workgroup)
@@ -251,7 +304,8 @@ size_t sky_scratch_bytes(Geom g) {
            + 4 * kSkyT * W                       // borders per threshold
            + 3 * 4 * kSkyT * W                   // sky moments per threshold
            + 2 * 4 * W                           // dark rows, final border
-           + npx;                                // gray image
+           + npx                                 // gray image
+           + 64 + 24 * (size_t)((g.W + 63) / 64) * ((g.H + 15) / 16);  // gray partials
 }
 
 hipError_t launch_sky_detect(const uint8_t *img, int pitch, uint8_t *mask, int mask_pitch,
@@ -265,14 +319,22 @@ hipError_t launch_sky_detect(const uint8_t *img, int pitch, uint8_t *mask, int m
     int *M = (int *)p;             p += 3 * 4 * kSkyT * W;
     int *dark = (int *)p;          p += 4 * W;
     int *border = (int *)p;        p += 4 * W;
-    uint8_t *G = (uint8_t *)p;
-    hipError_t e = hipMemsetAsync(tot, 0, 8 * 3 * (kSkyT + 1), st);
+    uint8_t *G = (uint8_t *)p;     p += (size_t)g.H * W;
+    long long *partial = (long long *)(((uintptr_t)p + 63) & ~(uintptr_t)63);
+    const dim3 gridg((g.W + 63) / 64, (g.H + 15) / 16);
+    hipLaunchKernelGGL(sky_gray_kernel, gridg, dim3(256), 0, st, img, pitch, g.scale, G, g.H, g.W,
+                       partial);
+    const int half = g.H / 2, last = half < g.H - 1 ? half : g.H - 1;
+    const size_t strip = (size_t)(last + 2) * kSkyStripW;
+    if (strip > kSkyStripMax) return hipErrorInvalidValue;  // H > ~4700 rows
+    hipError_t e = hipFuncSetAttribute((const void *)sky_columns_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)strip);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + 63) / 64), dim3(256), strip, st, G, g.H,
+                       g.W, B, M, dark);
+    hipLaunchKernelGGL(sky_reduce_kernel, dim3(kSkyT + 1), dim3(256), 0, st, M, g.W, partial,
+                       (int)(gridg.x * gridg.y), tot);
     const dim3 grid2((g.W + 63) / 64, (g.H + 3) / 4);
-    hipLaunchKernelGGL(sky_gray_kernel, grid2, dim3(256), 0, st, img, pitch, g.scale, G, g.H, g.W,
-                       tot);
-    hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + 63) / 64), dim3(64), 0, st, G, g.H, g.W, B,
-                       M, dark, tot);
     hipLaunchKernelGGL(sky_select_kernel, dim3(1), dim3(1024), 0, st, B, dark, tot, g.H, g.W,
                        border);
     hipLaunchKernelGGL(sky_mask_kernel, grid2, dim3(256), 0, st, border, g.H, g.W, mask,
