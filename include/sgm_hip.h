@@ -82,7 +82,18 @@ typedef struct sgm_params {
                           WTA disparity as float (BM.cpp:53-85; post_filter()ed when
                           post_filter is set, BM.cpp:88), raw_disp = the same as u16;
                           views, lk_refine and the right sky mask are unused */
+    int aux_only;      /* 1: a light handle for the per-frame side stages only (sky detector,
+                          post_filter, LKRefine, colormap, point cloud): no cost volumes are
+                          allocated and sgm_process[_device] refuse; 0 (default) */
 } sgm_params;
+
+/* Camera of the point cloud (CamIntrinsics, inc/utils.h:14-20, plus the two
+ * constants of node.cpp:122-123). */
+typedef struct sgm_camera {
+    float fx, fy, cx, cy;
+    double baseline;   /* 0.5 in node.cpp:123 */
+    float max_range;   /* 100 in node.cpp:122 */
+} sgm_camera;
 
 typedef struct sgm_handle sgm_handle;
 
@@ -161,6 +172,23 @@ int sgm_lk_refine_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_
 int sgm_sky_detect_device(sgm_handle *h, const uint8_t *d_img, int pitch, uint8_t *d_mask,
                           int mask_pitch, void *stream);
 
+/* Solver::colormap (src/Solver.cpp:652-707) of a DEVICE working-grid map
+ * (rows x cols f32, pitch in floats) into DEVICE BGR (rows x cols x 3 u8,
+ * bgr_pitch bytes): the image show_disp publishes (Solver.cpp:55-93). */
+int sgm_colormap_device(sgm_handle *h, const float *d_disp, int pitch, uint8_t *d_bgr,
+                        int bgr_pitch, void *stream);
+
+/* The point cloud of node.cpp:119-143 from a DEVICE working-grid map: every
+ * pixel with disp != D+1 and Z = (fx+fy)/2 * baseline / (disp + 1e-6) <=
+ * max_range becomes (X, Y, Z) (doubles) and the gray value img(i, j) of the
+ * DEVICE image d_img (img_pitch bytes; the node reads its full-size image
+ * at working-grid indices, node.cpp:137), in row-major order.  d_xyz holds
+ * up to rows*cols*3 doubles, d_pixel rows*cols bytes; *d_count (device int)
+ * receives the number of points.  Enqueued on `stream`. */
+int sgm_point_cloud_device(sgm_handle *h, const float *d_disp, int pitch, const uint8_t *d_img,
+                           int img_pitch, const sgm_camera *cam, double *d_xyz,
+                           uint8_t *d_pixel, int *d_count, void *stream);
+
 /* ---- per-kernel timing (HIP events recorded around every launch) ---- */
 
 typedef struct sgm_kernel_stat {
@@ -205,6 +233,13 @@ int sgm_stage_lk_refine(sgm_handle *h, const uint8_t *left, const uint8_t *right
 /* Sky detector (sgm_sky_detect_device) with HOST buffers: img full-size
  * (pitch bytes), mask rows x cols; synchronous. */
 int sgm_stage_sky_detect(sgm_handle *h, const uint8_t *img, int pitch, uint8_t *mask);
+/* colormap with HOST buffers: disp rows x cols, bgr rows x cols x 3. */
+int sgm_stage_colormap(sgm_handle *h, const float *disp, uint8_t *bgr);
+/* point cloud with HOST buffers: disp rows x cols, img the full-size image
+ * (img_pitch bytes); xyz (3*rows*cols doubles) and pixel (rows*cols) receive
+ * *count points. */
+int sgm_stage_point_cloud(sgm_handle *h, const float *disp, const uint8_t *img, int img_pitch,
+                          const sgm_camera *cam, double *xyz, uint8_t *pixel, int *count);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,8 @@ EXPORTS = (
     "sgm_post_filter_device", "sgm_stage_census", "sgm_stage_cost", "sgm_stage_path",
     "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
     "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine", "sgm_sky_detect_device",
-    "sgm_stage_sky_detect",
+    "sgm_stage_sky_detect", "sgm_colormap_device", "sgm_point_cloud_device", "sgm_stage_colormap",
+    "sgm_stage_point_cloud",
 )
 
 
@@ -45,8 +46,15 @@ class Params(ctypes.Structure):
         ("uniqueness", ctypes.c_float), ("lr_max_diff", ctypes.c_float),
         ("blur", ctypes.c_int), ("views", ctypes.c_int), ("post_filter", ctypes.c_int),
         ("lk_refine", ctypes.c_int), ("sky_detect", ctypes.c_int),
-        ("solver", ctypes.c_int),
+        ("solver", ctypes.c_int), ("aux_only", ctypes.c_int),
     ]
+
+
+class Camera(ctypes.Structure):
+    """sgm_camera: CamIntrinsics (inc/utils.h:14-20) + node.cpp:122-123."""
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float),
+                ("cy", ctypes.c_float), ("baseline", ctypes.c_double),
+                ("max_range", ctypes.c_float)]
 
 
 class KernelStat(ctypes.Structure):
@@ -94,6 +102,11 @@ def lib():
     L.sgm_stage_lk_refine.argtypes = [P, P, P, I, P]
     L.sgm_sky_detect_device.argtypes = [P, P, I, P, I, P]
     L.sgm_stage_sky_detect.argtypes = [P, P, I, P]
+    CP = ctypes.POINTER(Camera)
+    L.sgm_colormap_device.argtypes = [P, P, I, P, I, P]
+    L.sgm_point_cloud_device.argtypes = [P, P, I, P, I, CP, P, P, P, P]
+    L.sgm_stage_colormap.argtypes = [P, P, P]
+    L.sgm_stage_point_cloud.argtypes = [P, P, P, I, CP, P, P, P]
     L.sgm_stage_census.argtypes = [P, P, I, P]
     L.sgm_stage_cost.argtypes = [P, P, P, P, I, I, P]
     L.sgm_stage_path.argtypes = [P, I, P, P, P]

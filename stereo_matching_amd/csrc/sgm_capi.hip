@@ -61,6 +61,7 @@ struct sgm_handle {
     int pf_iters;         // median launches of the last post filter
     float *d_lk_in;       // LKRefine input copy (the kernel refines the map in place)
     uint8_t *d_sky_scratch;  // sky detector scratch (sgm_sky.hip)
+    int *d_cloud_counts;  // point cloud: per-row counts -> offsets, then the total
     uint8_t *h_pin;       // pinned host staging for sgm_process (allocated on first use)
     size_t h_pin_bytes;
     char err[512];
@@ -151,6 +152,7 @@ void free_all(sgm_handle *h) {
     (void)hipFree(h->d_pf_changes);
     (void)hipFree(h->d_lk_in);
     (void)hipFree(h->d_sky_scratch);
+    (void)hipFree(h->d_cloud_counts);
     if (h->h_pf_changes) (void)hipHostFree(h->h_pf_changes);
     h->h_pf_changes = nullptr;
     (void)hipFree(h->d_min);
@@ -529,6 +531,7 @@ int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
     p->lk_refine = 0;        // 1: + LKRefine (SGM.cpp:824, commented out in the reference)
     p->sky_detect = 0;       // 1: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
     p->solver = SGM_SOLVER_SGM;
+    p->aux_only = 0;
     return SGM_OK;
 }
 
@@ -580,7 +583,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if ((rc = dalloc(h, &h->d_sky[v], npx))) break;
             if ((rc = dalloc(h, &h->d_ct[v], npx))) break;
         }
-        for (int v = 0; v < h->nviews && !rc; ++v) {
+        for (int v = 0; v < (p->aux_only ? 0 : h->nviews) && !rc; ++v) {
             if ((rc = dalloc(h, &h->d_ch[v], nvol))) break;
             // + guard: the row-walking forward pass prefetches up to PF
             // positions past the end of the last row (never consumed)
@@ -591,9 +594,15 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             for (int f = 0; f < 3 && !rc; ++f)
                 rc = dalloc(h, &h->d_ck[v][f], sgm::pair_ckpt_floats(f, h->g));
         }
-        if (!rc && h->nviews == 1) {  // stage_lr needs a second sub-pixel map
+        if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
+            for (int v = 0; v < 2 && !rc; ++v) {
+                if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
+                rc = dalloc(h, &h->d_sub[v], npx);
+            }
+        } else if (!rc && h->nviews == 1) {  // stage_lr needs a second sub-pixel map
             rc = dalloc(h, &h->d_sub[1], npx);
         }
+        if (!rc) rc = dalloc(h, &h->d_cloud_counts, (size_t)h->g.H + 1);
         if (!rc) rc = dalloc(h, &h->d_out, npx);
         if (!rc) rc = dalloc(h, &h->d_min, npx);
         if (!rc) rc = dalloc(h, &h->d_zero, 256);
@@ -652,6 +661,8 @@ int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_ri
     if (!d_left || !d_right || !d_out || pitch < h->p.width || out_pitch < h->g.W ||
         ((d_sky_l || d_sky_r) && sky_pitch < h->g.W))
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process_device: bad pointer or pitch");
+    if (h->p.aux_only)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process_device: handle created with aux_only");
     DeviceGuard guard(h->device);
     hipStream_t st = stream ? (hipStream_t)stream : h->st;
     return run_frame(h, d_left, d_right, pitch, d_sky_l, d_sky_r, sky_pitch, d_out, out_pitch,
@@ -665,6 +676,8 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
     if (!left || !right || !out || pitch < h->p.width || out_pitch < h->g.W ||
         ((sky_l || sky_r) && sky_pitch < h->g.W))
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: bad pointer or pitch");
+    if (h->p.aux_only)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: handle created with aux_only");
     DeviceGuard guard(h->device);
     int rc;
     if ((rc = ensure_pinned(h))) return rc;
@@ -800,6 +813,7 @@ int sgm_stage_census(sgm_handle *h, const uint8_t *img, int pitch, uint64_t *ct)
 int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                    int view, int filters, float *cost) {
     if (!h || !ctl || !ctr || !cost || (view != 0 && view != 1)) return SGM_ERR_INVALID_ARG;
+    if (h->p.aux_only) return set_err(h, SGM_ERR_INVALID_ARG, "stage needs cost volumes (aux_only)");
     DeviceGuard guard(h->device);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_ct[0], ctl, npx * 8, hipMemcpyHostToDevice, h->st));
@@ -821,6 +835,7 @@ int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr, cons
 
 int sgm_stage_path(sgm_handle *h, int dir, const float *cost, float *L, float *minL) {
     if (!h || !cost || !L || dir < 0 || dir > 7) return SGM_ERR_INVALID_ARG;
+    if (h->p.aux_only) return set_err(h, SGM_ERR_INVALID_ARG, "stage needs cost volumes (aux_only)");
     DeviceGuard guard(h->device);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
@@ -837,6 +852,7 @@ int sgm_stage_path(sgm_handle *h, int dir, const float *cost, float *L, float *m
 
 int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float *sub) {
     if (!h || !cost) return SGM_ERR_INVALID_ARG;
+    if (h->p.aux_only) return set_err(h, SGM_ERR_INVALID_ARG, "stage needs cost volumes (aux_only)");
     DeviceGuard guard(h->device);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
@@ -908,6 +924,88 @@ int sgm_stage_sky_detect(sgm_handle *h, const uint8_t *img, int pitch, uint8_t *
     HIPCHK(h, hipMemcpyAsync(mask, h->d_sky[0], npx, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return SGM_OK;
+}
+
+int sgm_colormap_device(sgm_handle *h, const float *d_disp, int pitch, uint8_t *d_bgr,
+                        int bgr_pitch, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!d_disp || !d_bgr || pitch < h->g.W || bgr_pitch < 3 * h->g.W)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_colormap_device: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    HIPCHK(h, timed(h, "colormap", (double)h->g.H * h->g.W, st, [&] {
+               return sgm::launch_colormap(d_disp, pitch, d_bgr, bgr_pitch, h->g, st);
+           }));
+    return SGM_OK;
+}
+
+int sgm_point_cloud_device(sgm_handle *h, const float *d_disp, int pitch, const uint8_t *d_img,
+                           int img_pitch, const sgm_camera *cam, double *d_xyz,
+                           uint8_t *d_pixel, int *d_count, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    if (!d_disp || !d_img || !cam || !d_xyz || !d_pixel || !d_count || pitch < h->g.W ||
+        img_pitch < h->g.W)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_point_cloud_device: bad pointer or pitch");
+    DeviceGuard guard(h->device);
+    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    HIPCHK(h, timed(h, "point_cloud", (double)h->g.H * h->g.W, st, [&] {
+               return sgm::launch_point_cloud(d_disp, pitch, d_img, img_pitch, cam->fx, cam->fy,
+                                              cam->cx, cam->cy, cam->baseline, cam->max_range,
+                                              h->d_cloud_counts, d_xyz, d_pixel, d_count, h->g,
+                                              st);
+           }));
+    return SGM_OK;
+}
+
+int sgm_stage_colormap(sgm_handle *h, const float *disp, uint8_t *bgr) {
+    if (!h || !disp || !bgr) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    // staging: the map in d_out, the BGR image over the two working-grid sky masks' space
+    uint8_t *d_bgr = nullptr;
+    HIPCHK(h, hipMallocAsync((void **)&d_bgr, 3 * npx, h->st));
+    HIPCHK(h, hipMemcpyAsync(h->d_out, disp, npx * 4, hipMemcpyHostToDevice, h->st));
+    int rc = sgm_colormap_device(h, h->d_out, h->g.W, d_bgr, 3 * h->g.W, h->st);
+    if (!rc) {
+        HIPCHK(h, hipMemcpyAsync(bgr, d_bgr, 3 * npx, hipMemcpyDeviceToHost, h->st));
+    }
+    HIPCHK(h, hipFreeAsync(d_bgr, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return rc;
+}
+
+int sgm_stage_point_cloud(sgm_handle *h, const float *disp, const uint8_t *img, int img_pitch,
+                          const sgm_camera *cam, double *xyz, uint8_t *pixel, int *count) {
+    if (!h || !disp || !img || !cam || !xyz || !pixel || !count || img_pitch < h->g.W)
+        return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    const size_t npx = (size_t)h->g.H * h->g.W;
+    const int rows_used = h->g.H;  // the node reads img(i, j) at working-grid indices
+    uint8_t *d_img = nullptr, *d_pix = nullptr;
+    double *d_xyz = nullptr;
+    int *d_n = nullptr;
+    HIPCHK(h, hipMallocAsync((void **)&d_img, (size_t)rows_used * img_pitch, h->st));
+    HIPCHK(h, hipMallocAsync((void **)&d_pix, npx, h->st));
+    HIPCHK(h, hipMallocAsync((void **)&d_xyz, 3 * npx * sizeof(double), h->st));
+    HIPCHK(h, hipMallocAsync((void **)&d_n, sizeof(int), h->st));
+    HIPCHK(h, hipMemcpyAsync(d_img, img, (size_t)rows_used * img_pitch, hipMemcpyHostToDevice,
+                             h->st));
+    HIPCHK(h, hipMemcpyAsync(h->d_out, disp, npx * 4, hipMemcpyHostToDevice, h->st));
+    int rc = sgm_point_cloud_device(h, h->d_out, h->g.W, d_img, img_pitch, cam, d_xyz, d_pix, d_n,
+                                    h->st);
+    if (!rc) {
+        HIPCHK(h, hipMemcpyAsync(count, d_n, sizeof(int), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipStreamSynchronize(h->st));
+        HIPCHK(h, hipMemcpyAsync(xyz, d_xyz, 3 * (size_t)*count * sizeof(double),
+                                 hipMemcpyDeviceToHost, h->st));
+        HIPCHK(h, hipMemcpyAsync(pixel, d_pix, (size_t)*count, hipMemcpyDeviceToHost, h->st));
+    }
+    HIPCHK(h, hipFreeAsync(d_img, h->st));
+    HIPCHK(h, hipFreeAsync(d_pix, h->st));
+    HIPCHK(h, hipFreeAsync(d_xyz, h->st));
+    HIPCHK(h, hipFreeAsync(d_n, h->st));
+    HIPCHK(h, hipStreamSynchronize(h->st));
+    return rc;
 }
 
 int sgm_stage_post_filter(sgm_handle *h, float *disp) {

@@ -107,6 +107,13 @@ hipError_t launch_lk_refine(const uint8_t *left, const uint8_t *right, int pitch
 size_t sky_scratch_bytes(Geom g);
 hipError_t launch_sky_detect(const uint8_t *img, int pitch, uint8_t *mask, int mask_pitch,
                              void *scratch, Geom g, hipStream_t st);
+// consumers (sgm_consumers.hip): Solver::colormap and the node's point cloud
+hipError_t launch_colormap(const float *disp, int pitch, uint8_t *bgr, int bgr_pitch, Geom g,
+                           hipStream_t st);
+hipError_t launch_point_cloud(const float *disp, int pitch, const uint8_t *img, int img_pitch,
+                              float fx, float fy, float cx, float cy, double baseline,
+                              float max_range, int *counts, double *xyz, uint8_t *pixel,
+                              int *total, Geom g, hipStream_t st);
 hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
                      Geom g, hipStream_t st);
 

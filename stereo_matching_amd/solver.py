@@ -37,7 +37,7 @@ class SGM:
                  blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
                  uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False,
                  lk_refine: bool = False, sky_detect: bool = False,
-                 _solver: int = _capi.SGM_SOLVER_SGM):
+                 aux_only: bool = False, _solver: int = _capi.SGM_SOLVER_SGM):
         self._lib = lib()
         p = _capi.default_params(h, w, s, d)
         p.blur = int(bool(blur))
@@ -50,6 +50,8 @@ class SGM:
         # sky_detect: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
         p.sky_detect = int(bool(sky_detect))
         p.solver = _solver
+        # aux_only: side stages only (sky, post_filter, LKRefine, colormap, cloud)
+        p.aux_only = int(bool(aux_only))
         p.p1, p.p2 = p1, p2
         p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
         self.params = p
@@ -173,6 +175,31 @@ class SGM:
         check(self._lib.sgm_sky_detect_device(self._h, ctypes.c_void_p(d_img), pitch or self.w,
                                               ctypes.c_void_p(d_mask), mask_pitch or self.cols,
                                               ctypes.c_void_p(stream or None)), self._h)
+
+    def colormap(self, disp) -> np.ndarray:
+        """Solver::colormap (Solver.cpp:652-707) on the GPU: rows x cols x 3 BGR."""
+        f = np.ascontiguousarray(disp, dtype=np.float32)
+        if f.shape != (self.rows, self.cols):
+            raise ValueError(f"disp: expected shape {(self.rows, self.cols)}, got {f.shape}")
+        out = np.empty((self.rows, self.cols, 3), np.uint8)
+        check(self._lib.sgm_stage_colormap(self._h, _ptr(f), _ptr(out)), self._h)
+        return out
+
+    def point_cloud(self, disp, img, fx, fy, cx, cy, baseline=0.5, max_range=100.0):
+        """node.cpp:119-143 on the GPU: (N x 3 float64 points, N u8 gray values)
+        in row-major order; img is the node's full-size image."""
+        f = np.ascontiguousarray(disp, dtype=np.float32)
+        im = np.ascontiguousarray(img, dtype=np.uint8)
+        if f.shape != (self.rows, self.cols) or im.shape[0] < self.rows or im.shape[1] < self.cols:
+            raise ValueError("disp must be rows x cols and img at least that large")
+        cam = _capi.Camera(fx, fy, cx, cy, baseline, max_range)
+        xyz = np.empty((self.rows * self.cols, 3), np.float64)
+        pix = np.empty(self.rows * self.cols, np.uint8)
+        n = ctypes.c_int()
+        check(self._lib.sgm_stage_point_cloud(self._h, _ptr(f), _ptr(im), im.shape[1],
+                                              ctypes.byref(cam), _ptr(xyz), _ptr(pix),
+                                              ctypes.byref(n)), self._h)
+        return xyz[:n.value].copy(), pix[:n.value].copy()
 
     def get_raw_disp(self) -> np.ndarray:
         """Left WTA disparity (SGM.cpp:411-415), uint16, invalid = D+1."""

@@ -4,8 +4,12 @@
 //   sgm_class_surface nodevice            -> argument asserts + no-device error
 //   sgm_class_surface run L R H W D OUT   -> raw u8 pair in, f32 disparity out
 //   sgm_class_surface runbm L R H W D OUT -> the same through BM(h, w, s, d)
+//   sgm_class_surface sky IMG H W S OUT   -> SkyAreaDetector::detect mask
+//   sgm_class_surface lk L R DISP H W D OUT -> LKSubPixel::LKRefine of DISP
 #define SGM_AMD_THROW 1
 #include "sgm_amd/SGM.h"
+#include "sgm_amd/LKSubPixel.h"
+#include "sgm_amd/SkyAreaDetector.h"
 
 #include <cstdio>
 #include <fstream>
@@ -60,6 +64,36 @@ int main(int argc, char **argv) {
             fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
         return fo ? 0 : 4;
     }
-    std::fprintf(stderr, "usage: %s nodevice | run|runbm L R H W D OUT\n", argv[0]);
+    if (argc == 7 && std::string(argv[1]) == "sky") {
+        const int h = std::atoi(argv[3]), w = std::atoi(argv[4]), s = std::atoi(argv[5]);
+        Mat img(h, w, CV_8UC1), mask;
+        std::ifstream fi(argv[2], std::ios::binary);
+        fi.read(reinterpret_cast<char *>(img.data), (std::streamsize)h * w);
+        if (!fi) return 2;
+        sky_detector::SkyAreaDetector det;
+        det.detect(img, "unused.png", mask, s);
+        det.detect(img, "unused.png", mask, s);  // the handle is reused
+        if (mask.rows != h / s || mask.cols != w / s || mask.type() != CV_8UC1) return 3;
+        std::ofstream fo(argv[6], std::ios::binary);
+        fo.write(reinterpret_cast<const char *>(mask.data), (std::streamsize)mask.rows * mask.cols);
+        return fo ? 0 : 4;
+    }
+    if (argc == 9 && std::string(argv[1]) == "lk") {
+        const int h = std::atoi(argv[5]), w = std::atoi(argv[6]), d = std::atoi(argv[7]);
+        Mat l(h, w, CV_8UC1), r(h, w, CV_8UC1), disp(h, w, CV_32FC1);
+        std::ifstream fl(argv[2], std::ios::binary), fr(argv[3], std::ios::binary),
+            fd(argv[4], std::ios::binary);
+        fl.read(reinterpret_cast<char *>(l.data), (std::streamsize)h * w);
+        fr.read(reinterpret_cast<char *>(r.data), (std::streamsize)h * w);
+        fd.read(reinterpret_cast<char *>(disp.data), (std::streamsize)h * w * 4);
+        if (!fl || !fr || !fd) return 2;
+        sgm_amd::LKSubPixelPtr lk = sgm_amd::LKSubPixel::create(h, w, 1, d);
+        lk->LKRefine(l, r, disp);
+        std::ofstream fo(argv[8], std::ios::binary);
+        fo.write(reinterpret_cast<const char *>(disp.data), (std::streamsize)h * w * 4);
+        return fo ? 0 : 4;
+    }
+    std::fprintf(stderr, "usage: %s nodevice | run|runbm L R H W D OUT | sky IMG H W S OUT | "
+                 "lk L R DISP H W D OUT\n", argv[0]);
     return 2;
 }

@@ -413,3 +413,53 @@ def bm_process(left, right, D, scale=1, sky=None, uniq=0.7, blur_on=True):
                     d = D + 1
             disp[i, j] = d
     return disp
+
+
+def colormap(F, D):
+    """Solver::colormap (src/Solver.cpp:652-707): BGR u8, float32 arithmetic,
+    float -> uchar conversions truncating, the last two bands in double."""
+    F = np.asarray(F, np.float32)
+    H, W = F.shape
+    out = np.zeros((H, W, 3), np.uint8)
+    for i in range(H):
+        for j in range(W):
+            v = F[i, j]
+            if v > D - 1:
+                continue
+            v = f32(v * f32(256 // D))
+            if v <= 51:
+                out[i, j] = (255, int(f32(v * f32(5))), 0)
+            elif v <= 102:
+                v = f32(v - f32(51))
+                out[i, j] = (int(f32(f32(255) - f32(v * f32(5)))), 255, 0)
+            elif v <= 153:
+                v = f32(v - f32(102))
+                out[i, j] = (0, 255, int(f32(v * f32(5))))
+            elif v <= 204:
+                v = f32(v - f32(153))
+                out[i, j] = (0, 255 - int(128.0 * float(v) / 51.0 + 0.5), 255)
+            else:
+                v = f32(v - f32(204))
+                out[i, j] = (0, 127 - int(127.0 * float(v) / 51.0 + 0.5), 255)
+    return out
+
+
+def point_cloud(F, img, D, scale, fx, fy, cx, cy, baseline=0.5, max_range=100.0):
+    """node.cpp:119-143: row-major (X, Y, Z) doubles and img(i, j) gray values."""
+    F = np.asarray(F, np.float32)
+    H, W = F.shape
+    fx, fy, cx, cy, mr = f32(fx), f32(fy), f32(cx), f32(cy), f32(max_range)
+    pts, pix = [], []
+    for i in range(H):
+        for j in range(W):
+            d = F[i, j]
+            if d == f32(D + 1):
+                continue
+            Z = float(f32(fx + fy)) / 2.0 * baseline / (float(d) + 1e-6)
+            if Z > float(mr):
+                continue
+            X = float(f32(f32(j * scale) - cx)) * Z / float(fx)
+            Y = float(f32(f32(i * scale) - cy)) * Z / float(fy)
+            pts.append((X, Y, Z))
+            pix.append(int(img[i, j]))
+    return np.array(pts, np.float64).reshape(-1, 3), np.array(pix, np.uint8)

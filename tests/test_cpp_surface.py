@@ -78,3 +78,37 @@ def test_bm_class_surface_matches_oracle(exe, tmp_path):
     got = np.fromfile(fo, dtype=np.float32).reshape(h, w)
     want = oracle.post_filter(oracle.bm_process(left, right, D).astype(np.float32), D)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_sky_detector_wrapper_matches_reference_example(exe, tmp_path):
+    # sky_detector::SkyAreaDetector as node.cpp:51,83 uses it, on the
+    # reference's own example (tests/golden/sky_000017_14.npz)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "sky_000017_14.npz"))
+    img, want = g["image"], g["mask"]
+    fi, fo = str(tmp_path / "img.raw"), str(tmp_path / "mask.raw")
+    img.tofile(fi)
+    h, w = img.shape
+    r = subprocess.run([exe, "sky", fi, str(h), str(w), "1", fo], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert np.array_equal(np.fromfile(fo, np.uint8).reshape(h, w), want)
+
+
+@pytest.mark.gpu
+def test_lk_wrapper_matches_oracle(exe, tmp_path):
+    import oracle
+    oracle.build()
+    h, w, D = 64, 200, 64
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=5)
+    disp = oracle.process(left, right, D)["final"]
+    paths = [str(tmp_path / n) for n in ("l.raw", "r.raw", "d.raw", "out.raw")]
+    left.tofile(paths[0])
+    right.tofile(paths[1])
+    disp.tofile(paths[2])
+    r = subprocess.run([exe, "lk", *paths[:3], str(h), str(w), str(D), paths[3]],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(paths[3], np.float32).reshape(h, w)
+    want = oracle.lk_refine(left, right, disp, D)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
