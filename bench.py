@@ -83,7 +83,7 @@ BYTES_PER_PIXEL = {"census": 9, "lr": 12,
                    # the original and working maps (8); labelling reads the map and
                    # writes label + count (12); the area test reads map, 2 labels,
                    # area and writes the map (16); count/merge touch few pixels
-                   "post_median": 8, "post_cc_local": 12, "post_cc_apply": 16,
+                   "post_prep": 12, "post_median": 8, "post_cc_local": 16, "post_cc_apply": 20,
                    "post_cc_count": 4, "post_cc_merge": 0,
                    # LKRefine: map in + out, 7x7 window and images through LDS/L2
                    "lk_refine": 10,

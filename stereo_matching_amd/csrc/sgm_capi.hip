@@ -36,7 +36,7 @@ struct sgm_handle {
     size_t bytes;
     hipStream_t st;       // the handle's own stream (host API, stages)
     hipStream_t aux[1];      // right view (two-view frames)
-    hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1;
+    hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1, ev_pf;
     uint8_t *d_in[2];     // full-size input staging (host API)
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
@@ -164,7 +164,7 @@ void free_all(sgm_handle *h) {
     if (h->st) (void)hipStreamDestroy(h->st);
     for (auto &s : h->aux) if (s) (void)hipStreamDestroy(s);
     hipEvent_t evs[] = {h->ev_ct, h->ev_c[0], h->ev_c[1], h->ev_t[0], h->ev_t[1],
-                        h->ev_s[0], h->ev_s[1], h->ev_v1};
+                        h->ev_s[0], h->ev_s[1], h->ev_v1, h->ev_pf};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -327,7 +327,7 @@ int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int p
     const double npx = (double)g.H * g.W, elems = npx * g.D;
     if (h->p.sky_detect) {
         HIPCHK(h, timed(h, "sky_detect", npx, st, [&] {
-                   return sgm::launch_sky_detect(d_left, pitch, h->d_sky[0], g.W, h->d_sky_scratch,
+                   return sgm::launch_sky_detect(&d_left, pitch, h->d_sky, g.W, h->d_sky_scratch, 1,
                                                  g, st);
                }));
         d_sky_l = h->d_sky[0];
@@ -367,11 +367,11 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     hipStream_t aux1 = h->concurrent_views ? h->aux[0] : st;  // right view
     const double npx = (double)g.H * g.W;
     if (h->p.sky_detect) {  // node.cpp:80-93: detect on both inputs, then process with the masks
-        for (int v = 0; v < h->nviews; ++v)
-            HIPCHK(h, timed(h, "sky_detect", npx, st, [&] {
-                       return sgm::launch_sky_detect(v ? d_right : d_left, pitch, h->d_sky[v], g.W,
-                                                     h->d_sky_scratch, g, st);
-                   }));
+        const uint8_t *imgs[2] = {d_left, d_right};
+        HIPCHK(h, timed(h, "sky_detect", npx, st, [&] {
+                   return sgm::launch_sky_detect(imgs, pitch, h->d_sky, g.W, h->d_sky_scratch,
+                                                 h->nviews, g, st);
+               }));
         d_sky_l = h->d_sky[0];
         d_sky_r = h->nviews == 2 ? h->d_sky[1] : nullptr;
         sky_pitch = g.W;
@@ -449,17 +449,36 @@ void pack_rows(uint8_t *dst, const uint8_t *src, size_t row_bytes, int rows, siz
 
 // post_filter() (Solver.cpp:600-649) in place on a device map (sgm_post.hip):
 // median-fill launches until one changes nothing, then the speckle removal.
+// The fill works on a separate map and the component kernels write the
+// caller's map from it, so they are enqueued before the host reads the fill's
+// convergence counter (the GPU keeps working through that round trip); in the
+// rare case the fill had not converged, more fill launches run and the
+// component kernels are enqueued again.
 int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
     const Geom g = h->g;
-    const size_t npx = (size_t)g.H * g.W, row = (size_t)g.W * sizeof(float);
-    const double dnpx = (double)npx;
-    float *F = pitch == g.W ? d_map : h->d_pf_work;
-    HIPCHK(h, hipMemcpy2DAsync(h->d_pf_orig, row, d_map, (size_t)pitch * sizeof(float), row, g.H,
-                               hipMemcpyDeviceToDevice, st));
-    if (F != d_map)
-        HIPCHK(h, hipMemcpyAsync(F, h->d_pf_orig, npx * sizeof(float), hipMemcpyDeviceToDevice, st));
-    HIPCHK(h, hipMemsetAsync(h->d_pf_changes, 0, kMedianMaxLaunches * sizeof(int), st));
-    int k = 0;
+    const double dnpx = (double)g.H * g.W;
+    float *F = h->d_pf_work;
+    HIPCHK(h, timed(h, "post_prep", dnpx, st, [&] {
+               return sgm::launch_pf_prep(d_map, pitch, h->d_pf_orig, F, h->d_pf_changes,
+                                          kMedianMaxLaunches, g, st);
+           }));
+    auto components = [&]() -> int {
+        HIPCHK(h, timed(h, "post_cc_local", dnpx, st, [&] {
+                   return sgm::launch_cc_local(F, h->d_pf_label, h->d_pf_count, h->d_pf_area, g, st);
+               }));
+        HIPCHK(h, timed(h, "post_cc_merge", dnpx, st,
+                        [&] { return sgm::launch_cc_merge(F, h->d_pf_label, g, st); }));
+        HIPCHK(h, timed(h, "post_cc_count", dnpx, st, [&] {
+                   return sgm::launch_cc_count(h->d_pf_label, h->d_pf_count, h->d_pf_area, g, st);
+               }));
+        // speckle_filter_new(filtered_disp, invalid_disp, SPECKLE_SIZE/scale, SPECKLE_DIS), :645
+        HIPCHK(h, timed(h, "post_cc_apply", dnpx, st, [&] {
+                   return sgm::launch_cc_apply(F, h->d_pf_label, h->d_pf_area, 1000 / g.scale,
+                                               (float)(g.D + 1), d_map, pitch, g, st);
+               }));
+        return SGM_OK;
+    };
+    int k = 0, rc;
     for (;;) {
         // a fill usually settles in 2 launches and the 3rd proves it
         const int batch = k == 0 ? 3 : 2;
@@ -470,29 +489,15 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
                    }));
         HIPCHK(h, hipMemcpyAsync(h->h_pf_changes, h->d_pf_changes + k - 1, sizeof(int),
                                  hipMemcpyDeviceToHost, st));
-        HIPCHK(h, hipStreamSynchronize(st));
+        HIPCHK(h, hipEventRecord(h->ev_pf, st));
+        if ((rc = components())) return rc;
+        HIPCHK(h, hipEventSynchronize(h->ev_pf));
         if (*h->h_pf_changes == 0) break;
-        if (k + 3 > kMedianMaxLaunches)
+        if (k + 2 > kMedianMaxLaunches)
             return set_err(h, SGM_ERR_HIP, "post_filter: median fill did not converge in %d launches",
                            k);
     }
     h->pf_iters = k;
-    HIPCHK(h, timed(h, "post_cc_local", dnpx, st,
-                    [&] { return sgm::launch_cc_local(F, h->d_pf_label, h->d_pf_count, g, st); }));
-    HIPCHK(h, timed(h, "post_cc_merge", dnpx, st,
-                    [&] { return sgm::launch_cc_merge(F, h->d_pf_label, g, st); }));
-    HIPCHK(h, hipMemsetAsync(h->d_pf_area, 0, npx * sizeof(int), st));
-    HIPCHK(h, timed(h, "post_cc_count", dnpx, st, [&] {
-               return sgm::launch_cc_count(h->d_pf_label, h->d_pf_count, h->d_pf_area, g, st);
-           }));
-    // speckle_filter_new(filtered_disp, invalid_disp, SPECKLE_SIZE/scale, SPECKLE_DIS), :645
-    HIPCHK(h, timed(h, "post_cc_apply", dnpx, st, [&] {
-               return sgm::launch_cc_apply(F, h->d_pf_label, h->d_pf_area, 1000 / g.scale,
-                                           (float)(g.D + 1), g, st);
-           }));
-    if (F != d_map)
-        HIPCHK(h, hipMemcpy2DAsync(d_map, (size_t)pitch * sizeof(float), F, row, row, g.H,
-                                   hipMemcpyDeviceToDevice, st));
     return SGM_OK;
 }
 
@@ -574,7 +579,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
         if (rc) break;
         hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1],
-                             &h->ev_s[0], &h->ev_s[1], &h->ev_v1};
+                             &h->ev_s[0], &h->ev_s[1], &h->ev_v1, &h->ev_pf};
         for (auto e : evs)
             if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { rc = SGM_ERR_HIP; break; }
         if (rc) break;
@@ -613,7 +618,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         if (!rc) rc = dalloc(h, &h->d_pf_area, npx);
         if (!rc) rc = dalloc(h, &h->d_pf_snap, sgm::post_snapshot_floats(h->g));
         if (!rc) rc = dalloc(h, &h->d_lk_in, npx);
-        if (!rc) rc = dalloc(h, &h->d_sky_scratch, sgm::sky_scratch_bytes(h->g));
+        if (!rc) rc = dalloc(h, &h->d_sky_scratch, 2 * sgm::sky_scratch_bytes(h->g));
         if (!rc) rc = dalloc(h, &h->d_pf_changes, (size_t)kMedianMaxLaunches);
         if (!rc && hipHostMalloc((void **)&h->h_pf_changes, sizeof(int), hipHostMallocDefault) !=
                        hipSuccess)
@@ -907,8 +912,8 @@ int sgm_sky_detect_device(sgm_handle *h, const uint8_t *d_img, int pitch, uint8_
     DeviceGuard guard(h->device);
     hipStream_t st = stream ? (hipStream_t)stream : h->st;
     HIPCHK(h, timed(h, "sky_detect", (double)h->g.H * h->g.W, st, [&] {
-               return sgm::launch_sky_detect(d_img, pitch, d_mask, mask_pitch, h->d_sky_scratch,
-                                             h->g, st);
+               return sgm::launch_sky_detect(&d_img, pitch, &d_mask, mask_pitch, h->d_sky_scratch,
+                                             1, h->g, st);
            }));
     return SGM_OK;
 }

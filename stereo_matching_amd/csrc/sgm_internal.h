@@ -93,20 +93,23 @@ hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream
 size_t post_snapshot_floats(Geom g);
 hipError_t launch_median_fill(const float *orig, float *F, int iter, float *snap, int *changes,
                               Geom g, hipStream_t st);
-hipError_t launch_cc_local(const float *F, int *L, int *cnt, Geom g, hipStream_t st);
+hipError_t launch_pf_prep(const float *map, int pitch, float *orig, float *F, int *changes,
+                          int nchanges, Geom g, hipStream_t st);
+hipError_t launch_cc_local(const float *F, int *L, int *cnt, int *area, Geom g, hipStream_t st);
 hipError_t launch_cc_merge(const float *F, int *L, Geom g, hipStream_t st);
 hipError_t launch_cc_count(int *L, const int *cnt, int *area, Geom g, hipStream_t st);
-hipError_t launch_cc_apply(float *F, const int *L, const int *area, int max_size, float value,
-                           Geom g, hipStream_t st);
+hipError_t launch_cc_apply(const float *F, const int *L, const int *area, int max_size,
+                           float value, float *out, int out_pitch, Geom g, hipStream_t st);
 // LKRefine (sgm_lk.hip): left/right full-size images (decimated by g.scale on
 // the fly), din the working-grid map, dout (pitched) the refined map.
 hipError_t launch_lk_refine(const uint8_t *left, const uint8_t *right, int pitch, const float *din,
                             float *dout, int out_pitch, Geom g, hipStream_t st);
-// SkyAreaDetector::detect (sgm_sky.hip): img full-size (decimated by g.scale),
-// mask on the working grid; scratch of sky_scratch_bytes(g) bytes.
+// SkyAreaDetector::detect (sgm_sky.hip) on nviews (1 or 2) images at once:
+// img[v] full-size (decimated by g.scale), mask[v] on the working grid;
+// scratch of nviews * sky_scratch_bytes(g) bytes.
 size_t sky_scratch_bytes(Geom g);
-hipError_t launch_sky_detect(const uint8_t *img, int pitch, uint8_t *mask, int mask_pitch,
-                             void *scratch, Geom g, hipStream_t st);
+hipError_t launch_sky_detect(const uint8_t *const *img, int pitch, uint8_t *const *mask,
+                             int mask_pitch, void *scratch, int nviews, Geom g, hipStream_t st);
 // consumers (sgm_consumers.hip): Solver::colormap and the node's point cloud
 hipError_t launch_colormap(const float *disp, int pitch, uint8_t *bgr, int bgr_pitch, Geom g,
                            hipStream_t st);

@@ -7,9 +7,9 @@
 // not move between iterations -- the truncated disparities, the gradients
 // Ix = (L(j+1) - L(j-1)) * 0.5 and the left pixels -- are staged in LDS for
 // the tile plus a 3-pixel apron; the right-image samples R(m, n - d) move
-// with the offset and are gathered from global memory.  An iteration makes
-// three passes over the window: (A) validity, right samples and sum w^2, (B)
-// the Hessian, (C) the offset.  Zero-weight slots are skipped: adding +0 (or
+// with the offset and are gathered from global memory, all 49 in flight at
+// once, into registers.  An iteration makes three passes over the window:
+// (A) validity, sum w^2 and the right samples, (B) the Hessian, (C) the offset.  Zero-weight slots are skipped: adding +0 (or
 // -0) never changes an fp32 sum, so the sums equal the reference's 49-term
 // ones.
 #include "sgm_device.h"
@@ -29,7 +29,6 @@ __global__ __launch_bounds__(kLkThreads) void lk_refine_kernel(
     __shared__ float dtT[kLkAH][kLkAW];   // truncated disparity (interior), else as given
     __shared__ float ixT[kLkAH][kLkAW];   // gradient, 0 outside the interior
     __shared__ int lT[kLkAH][kLkAW];      // left pixel
-    __shared__ short resT[49][kLkThreads];  // Ires of the valid slots, per thread
 
     const int t = tid_x();
     const int i0 = bid_y() * kLkTH, j0 = bid_x() * kLkTW;
@@ -67,26 +66,33 @@ __global__ __launch_bounds__(kLkThreads) void lk_refine_kernel(
         const float wc2 = wc * wc;
         float last_disp = d0, last_doff = 0.f, last_diff = FLT_MAX;
         for (int it = 0; it < 10; ++it) {        // iter_num (LKSubPixelImpl.h:46)
-            // (A) the window (:114-163): valid slots, right samples, sum w^2
+            // (A) the window (:114-163): valid slots and sum w^2, then the
+            // right samples, all 49 loads issued before any is used
             unsigned long long valid = 0;
             int nvalid = 0;
             float s2 = 0.f;
+            int rx[49];
 #pragma unroll
             for (int k = 0; k < 49; ++k) {
                 const int v = k / 7 - kLkHW, u = k % 7 - kLkHW;
                 const float ix = ixT[ar + v][ac + u];
                 const float dm = dtT[ar + v][ac + u];
                 const int n = j + u;
-                const float dw = dm + last_doff;
-                const float x = (float)n - dw;
-                if (ix > 2.f && dm > 0.f && dm < fD && !(fabsf(d0 - dm) > 2.f) &&
-                    !(x < 0.f || x > (float)(W - 1))) {
-                    const uint8_t *rrow = right + (size_t)(i + v) * s * pitch;
-                    resT[k][t] = (short)((int)rrow[(size_t)(int)x * s] - lT[ar + v][ac + u]);
+                const float x = (float)n - (dm + last_doff);
+                const bool ok = ix > 2.f && dm > 0.f && dm < fD && !(fabsf(d0 - dm) > 2.f) &&
+                                !(x < 0.f || x > (float)(W - 1));
+                rx[k] = ok ? (int)x : j;  // a safe column for the skipped slots
+                if (ok) {
                     valid |= 1ull << k;
                     ++nvalid;
                     s2 += (v * v + u * u >= 18) ? wc2 : 1.f;
                 }
+            }
+            int rv[49];
+#pragma unroll
+            for (int k = 0; k < 49; ++k) {
+                const int v = k / 7 - kLkHW;
+                rv[k] = right[(size_t)(i + v) * s * pitch + (size_t)rx[k] * s];
             }
             if (nvalid < 5) break;               // valid_cnt < 4.9 (:165)
             const float nrm = sqrtf(s2);         // win_weight.norm() (:172)
@@ -109,7 +115,8 @@ __global__ __launch_bounds__(kLkThreads) void lk_refine_kernel(
                 if (!((valid >> k) & 1)) continue;
                 const int v = k / 7 - kLkHW, u = k % 7 - kLkHW;
                 const float ix = ixT[ar + v][ac + u];
-                doff += ((hinv * ix) * ((v * v + u * u >= 18) ? wnc : wn1)) * (float)resT[k][t];
+                const float res = (float)(rv[k] - lT[ar + v][ac + u]);  // Ires (:156)
+                doff += ((hinv * ix) * ((v * v + u * u >= 18) ? wnc : wn1)) * res;
             }
             if (fabsf(doff - last_doff) > last_diff) break;   // :201
             const float dn = d0 + doff;

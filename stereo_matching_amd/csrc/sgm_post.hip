@@ -249,7 +249,8 @@ __device__ void g_hook(int *L, int a, int b) {
 // need no union at all; runs of adjacent rows are then joined once per
 // contiguous overlap.
 __global__ __launch_bounds__(256) void cc_local_kernel(const float *__restrict__ F, int H, int W,
-                                                      int *__restrict__ L, int *__restrict__ cnt) {
+                                                      int *__restrict__ L, int *__restrict__ cnt,
+                                                      int *__restrict__ area) {
     __shared__ int lab[kCN];
     __shared__ int num[kCN];
     __shared__ float val[kCN];
@@ -261,6 +262,7 @@ __global__ __launch_bounds__(256) void cc_local_kernel(const float *__restrict__
         const int i = r0 + r, p = r * kCW + lane;
         val[p] = (i < H && j < W) ? F[(size_t)i * W + j] : 0.f;
         num[p] = 0;
+        if (i < H && j < W) area[(size_t)i * W + j] = 0;  // areas are indexed by root pixel
     }
     __syncthreads();
     for (int r = wave; r < kCH; r += 4) {
@@ -342,13 +344,29 @@ __global__ __launch_bounds__(256) void cc_count_kernel(int *L, const int *__rest
 
 // speckle_filter_new's last loop (:556-565): components of at most max_size
 // pixels become `value` (invalid_disp).
-__global__ __launch_bounds__(256) void cc_apply_kernel(float *F, const int *__restrict__ L,
-                                                      const int *__restrict__ area, int n,
-                                                      int max_size, float value) {
+__global__ __launch_bounds__(256) void cc_apply_kernel(const float *__restrict__ F,
+                                                      const int *__restrict__ L,
+                                                      const int *__restrict__ area, int n, int W,
+                                                      int max_size, float value,
+                                                      float *__restrict__ out, int out_pitch) {
     const int k = bid_x() * 256 + tid_x();
     if (k >= n) return;
     const int root = L[L[k]];  // L[k] is a (former) tile-local root, now flattened
-    if (area[root] <= max_size) F[k] = value;
+    out[(size_t)(k / W) * out_pitch + k % W] = area[root] <= max_size ? value : F[k];
+}
+
+// Entry of a post filter: the map (pitched) into the original and working
+// copies, and the fill's per-launch change counters zeroed.
+__global__ __launch_bounds__(256) void pf_prep_kernel(const float *__restrict__ map, int pitch,
+                                                     int H, int W, float *__restrict__ orig,
+                                                     float *__restrict__ F, int *changes,
+                                                     int nchanges) {
+    const int k = bid_x() * 256 + tid_x();
+    if (k < nchanges) changes[k] = 0;
+    if (k >= H * W) return;
+    const float v = map[(size_t)(k / W) * pitch + k % W];
+    orig[k] = v;
+    F[k] = v;
 }
 
 }  // namespace
@@ -365,9 +383,17 @@ hipError_t launch_median_fill(const float *orig, float *F, int iter, float *snap
     return hipGetLastError();
 }
 
-hipError_t launch_cc_local(const float *F, int *L, int *cnt, Geom g, hipStream_t st) {
+hipError_t launch_pf_prep(const float *map, int pitch, float *orig, float *F, int *changes,
+                          int nchanges, Geom g, hipStream_t st) {
+    const int n = g.H * g.W > nchanges ? g.H * g.W : nchanges;
+    hipLaunchKernelGGL(pf_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, map, pitch, g.H,
+                       g.W, orig, F, changes, nchanges);
+    return hipGetLastError();
+}
+
+hipError_t launch_cc_local(const float *F, int *L, int *cnt, int *area, Geom g, hipStream_t st) {
     const dim3 grid((g.W + kCW - 1) / kCW, (g.H + kCH - 1) / kCH);
-    hipLaunchKernelGGL(cc_local_kernel, grid, dim3(256), 0, st, F, g.H, g.W, L, cnt);
+    hipLaunchKernelGGL(cc_local_kernel, grid, dim3(256), 0, st, F, g.H, g.W, L, cnt, area);
     return hipGetLastError();
 }
 
@@ -383,11 +409,11 @@ hipError_t launch_cc_count(int *L, const int *cnt, int *area, Geom g, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_cc_apply(float *F, const int *L, const int *area, int max_size, float value,
-                           Geom g, hipStream_t st) {
+hipError_t launch_cc_apply(const float *F, const int *L, const int *area, int max_size,
+                           float value, float *out, int out_pitch, Geom g, hipStream_t st) {
     const int n = g.H * g.W;
     hipLaunchKernelGGL(cc_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, st, F, L, area, n,
-                       max_size, value);
+                       g.W, max_size, value, out, out_pitch);
     return hipGetLastError();
 }
 

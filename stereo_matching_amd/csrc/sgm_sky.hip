@@ -33,6 +33,21 @@ __device__ __forceinline__ long long sky_t2(int k) {  // t_k^2, t_k = 5 + 3k (:2
     return t * t;
 }
 
+// One detection's buffers; launches take both views and pick theirs by the
+// workgroup's z index (node.cpp:83-86 detects on both images).
+struct SkyView {
+    const uint8_t *img;
+    uint8_t *mask;
+    unsigned long long *tot;
+    int *B, *M, *dark, *border;
+    uint8_t *G;
+    long long *partial;
+};
+struct SkyViews {
+    SkyView v[2];
+};
+__device__ __forceinline__ int bid_z() { return (int)__builtin_amdgcn_workgroup_id_z(); }
+
 __device__ __forceinline__ long long wave_sum64(long long v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -41,9 +56,11 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
 
 // 1. working-grid gray image + moments of the non-zero pixels: 64 x 16
 // pixels per workgroup, one partial triple per workgroup (summed in 2b).
-__global__ __launch_bounds__(256) void sky_gray_kernel(const uint8_t *__restrict__ img, int pitch,
-                                                      int s, uint8_t *__restrict__ G, int H, int W,
-                                                      long long *partial) {
+__global__ __launch_bounds__(256) void sky_gray_kernel(SkyViews sv, int pitch, int s, int H, int W) {
+    const SkyView &V = sv.v[bid_z()];
+    const uint8_t *__restrict__ img = V.img;
+    uint8_t *__restrict__ G = V.G;
+    long long *partial = V.partial;
     __shared__ long long part[3][4];
     const int lane = tid_x() & 63, wave = tid_x() >> 6;
     const int j = bid_x() * 64 + lane;
@@ -85,10 +102,12 @@ __device__ __forceinline__ int reflect101(int x, int n) {  // BORDER_REFLECT_101
 // one lane per column.
 constexpr int kSkyStripW = 68;  // 66 window columns, then G[r][W-1], G[r][0]
 constexpr size_t kSkyStripMax = 160 * 1024 - 1024;
-__global__ __launch_bounds__(256) void sky_columns_kernel(const uint8_t *__restrict__ G, int H,
-                                                         int W, int *__restrict__ B,
-                                                         int *__restrict__ M,
-                                                         int *__restrict__ dark) {
+__global__ __launch_bounds__(256) void sky_columns_kernel(SkyViews sv, int H, int W) {
+    const SkyView &V = sv.v[bid_z()];
+    const uint8_t *__restrict__ G = V.G;
+    int *__restrict__ B = V.B;
+    int *__restrict__ M = V.M;
+    int *__restrict__ dark = V.dark;
     extern __shared__ uint8_t strip[];  // [rows 0..last+1][kSkyStripW]
     const int c0 = bid_x() * 64, t = tid_x();
     const int half = H / 2, last = half < H - 1 ? half : H - 1;
@@ -177,9 +196,11 @@ __global__ __launch_bounds__(256) void sky_columns_kernel(const uint8_t *__restr
 
 // 2b. per threshold k < kSkyT: the sums of the columns' sky moments; block
 // kSkyT: the image totals from the gray kernel's partials
-__global__ __launch_bounds__(256) void sky_reduce_kernel(const int *__restrict__ M, int W,
-                                                        const long long *__restrict__ partial,
-                                                        int npart, unsigned long long *tot) {
+__global__ __launch_bounds__(256) void sky_reduce_kernel(SkyViews sv, int W, int npart) {
+    const SkyView &V = sv.v[bid_z()];
+    const int *__restrict__ M = V.M;
+    const long long *__restrict__ partial = V.partial;
+    unsigned long long *tot = V.tot;
     __shared__ long long part[3][4];
     const int k = bid_x(), lane = tid_x() & 63, wave = tid_x() >> 6;
     const size_t kW = (size_t)kSkyT * W;
@@ -209,10 +230,12 @@ __global__ __launch_bounds__(256) void sky_reduce_kernel(const int *__restrict__
 }
 
 // 3. energies, the chosen border, the column checks (one workgroup)
-__global__ __launch_bounds__(1024) void sky_select_kernel(const int *__restrict__ B,
-                                                         const int *__restrict__ dark,
-                                                         const unsigned long long *tot, int H,
-                                                         int W, int *__restrict__ border) {
+__global__ __launch_bounds__(1024) void sky_select_kernel(SkyViews sv, int H, int W) {
+    const SkyView &V = sv.v[bid_z()];
+    const int *__restrict__ B = V.B;
+    const int *__restrict__ dark = V.dark;
+    const unsigned long long *tot = V.tot;
+    int *__restrict__ border = V.border;
     __shared__ double jn[kSkyT];
     __shared__ int kbest;
     __shared__ int bo[kSkyMaxW], bg[kSkyMaxW], bx[kSkyMaxW];
@@ -290,8 +313,10 @@ __global__ __launch_bounds__(1024) void sky_select_kernel(const int *__restrict_
 }
 
 // 4. make_sky_mask type 1 (:804-812)
-__global__ __launch_bounds__(256) void sky_mask_kernel(const int *__restrict__ border, int H, int W,
-                                                      uint8_t *__restrict__ mask, int pitch) {
+__global__ __launch_bounds__(256) void sky_mask_kernel(SkyViews sv, int H, int W, int pitch) {
+    const SkyView &V = sv.v[bid_z()];
+    const int *__restrict__ border = V.border;
+    uint8_t *__restrict__ mask = V.mask;
     const int j = bid_x() * 64 + (tid_x() & 63), i = bid_y() * 4 + (tid_x() >> 6);
     if (i < H && j < W) mask[(size_t)i * pitch + j] = i <= border[j] ? 255 : 0;
 }
@@ -308,37 +333,39 @@ size_t sky_scratch_bytes(Geom g) {
            + 64 + 24 * (size_t)((g.W + 63) / 64) * ((g.H + 15) / 16);  // gray partials
 }
 
-hipError_t launch_sky_detect(const uint8_t *img, int pitch, uint8_t *mask, int mask_pitch,
-                             void *scratch, Geom g, hipStream_t st) {
-    if (g.W > kSkyMaxW) return hipErrorInvalidValue;
+hipError_t launch_sky_detect(const uint8_t *const *img, int pitch, uint8_t *const *mask,
+                             int mask_pitch, void *scratch, int nviews, Geom g, hipStream_t st) {
+    if (g.W > kSkyMaxW || nviews < 1 || nviews > 2) return hipErrorInvalidValue;
     const size_t W = (size_t)g.W;
-    char *p = (char *)scratch;
-    unsigned long long *tot = (unsigned long long *)p;
-    p += kSkyTotBytes;
-    int *B = (int *)p;             p += 4 * kSkyT * W;
-    int *M = (int *)p;             p += 3 * 4 * kSkyT * W;
-    int *dark = (int *)p;          p += 4 * W;
-    int *border = (int *)p;        p += 4 * W;
-    uint8_t *G = (uint8_t *)p;     p += (size_t)g.H * W;
-    long long *partial = (long long *)(((uintptr_t)p + 63) & ~(uintptr_t)63);
-    const dim3 gridg((g.W + 63) / 64, (g.H + 15) / 16);
-    hipLaunchKernelGGL(sky_gray_kernel, gridg, dim3(256), 0, st, img, pitch, g.scale, G, g.H, g.W,
-                       partial);
+    SkyViews sv{};
+    for (int v = 0; v < nviews; ++v) {
+        char *p = (char *)scratch + v * sky_scratch_bytes(g);
+        SkyView &V = sv.v[v];
+        V.img = img[v];
+        V.mask = mask[v];
+        V.tot = (unsigned long long *)p;  p += kSkyTotBytes;
+        V.B = (int *)p;                   p += 4 * kSkyT * W;
+        V.M = (int *)p;                   p += 3 * 4 * kSkyT * W;
+        V.dark = (int *)p;                p += 4 * W;
+        V.border = (int *)p;              p += 4 * W;
+        V.G = (uint8_t *)p;               p += (size_t)g.H * W;
+        V.partial = (long long *)(((uintptr_t)p + 63) & ~(uintptr_t)63);
+    }
+    const dim3 gridg((g.W + 63) / 64, (g.H + 15) / 16, nviews);
+    hipLaunchKernelGGL(sky_gray_kernel, gridg, dim3(256), 0, st, sv, pitch, g.scale, g.H, g.W);
     const int half = g.H / 2, last = half < g.H - 1 ? half : g.H - 1;
     const size_t strip = (size_t)(last + 2) * kSkyStripW;
     if (strip > kSkyStripMax) return hipErrorInvalidValue;  // H > ~4700 rows
     hipError_t e = hipFuncSetAttribute((const void *)sky_columns_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)strip);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + 63) / 64), dim3(256), strip, st, G, g.H,
-                       g.W, B, M, dark);
-    hipLaunchKernelGGL(sky_reduce_kernel, dim3(kSkyT + 1), dim3(256), 0, st, M, g.W, partial,
-                       (int)(gridg.x * gridg.y), tot);
-    const dim3 grid2((g.W + 63) / 64, (g.H + 3) / 4);
-    hipLaunchKernelGGL(sky_select_kernel, dim3(1), dim3(1024), 0, st, B, dark, tot, g.H, g.W,
-                       border);
-    hipLaunchKernelGGL(sky_mask_kernel, grid2, dim3(256), 0, st, border, g.H, g.W, mask,
-                       mask_pitch);
+    hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + 63) / 64, 1, nviews), dim3(256), strip, st,
+                       sv, g.H, g.W);
+    hipLaunchKernelGGL(sky_reduce_kernel, dim3(kSkyT + 1, 1, nviews), dim3(256), 0, st, sv, g.W,
+                       (int)(gridg.x * gridg.y));
+    hipLaunchKernelGGL(sky_select_kernel, dim3(1, 1, nviews), dim3(1024), 0, st, sv, g.H, g.W);
+    hipLaunchKernelGGL(sky_mask_kernel, dim3((g.W + 63) / 64, (g.H + 3) / 4, nviews), dim3(256), 0,
+                       st, sv, g.H, g.W, mask_pitch);
     return hipGetLastError();
 }
 
