@@ -195,7 +195,10 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
         }
         sum -= a;
     };
-    // steps t < T-1 also add raw[WIN+t]; the last step only writes
+    // steps t < T-1 also add raw[WIN+t]; the last step only writes.  The
+    // next block's census words (and sky bytes) are loaded before the current
+    // block's steps run and only turned into costs after them, so the LDS
+    // round trips overlap the serial chain.
     int t = 0;
     float cur[U];
     if (T - 1 >= U) {
@@ -203,13 +206,23 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
         for (int u = 0; u < U; ++u) cur[u] = raw(WIN + u);
     }
     for (; t + 2 * U <= T - 1; t += U) {
-        float nxt[U];
+        uint64_t nl[U], nr[U];
+        uint8_t nk[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) nxt[u] = raw(WIN + t + U + u);
+        for (int u = 0; u < U; ++u) {
+            const int j = WIN + t + U + u;
+            nl[u] = word_l(j);
+            nr[u] = word_r(j);
+            if (SKY) nk[u] = sk[j];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) step(t + u, cur[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < U; ++u) {
+            const float c = hamming(nl[u], nr[u]);
+            if (SKY) cur[u] = nk[u] == 255 ? (d == 0 ? 0.0f : 999999.0f) : c;
+            else cur[u] = c;
+        }
     }
     if (t + U <= T - 1) {
 #pragma unroll
