@@ -333,11 +333,9 @@ int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int p
         d_sky_l = h->d_sky[0];
         sky_pitch = g.W;
     }
-    HIPCHK(h, timed(h, "census", npx, st, [&] {
-               return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st, true);
-           }));
-    HIPCHK(h, timed(h, "census", npx, st, [&] {
-               return sgm::launch_census(d_right, pitch, g, h->p.blur, h->d_ct[1], st, true);
+    HIPCHK(h, timed(h, "census", 2 * npx, st, [&] {
+               return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st, true, d_right,
+                                         h->d_ct[1]);
            }));
     int rc;
     if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
@@ -376,11 +374,9 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         d_sky_r = h->nviews == 2 ? h->d_sky[1] : nullptr;
         sky_pitch = g.W;
     }
-    HIPCHK(h, timed(h, "census", npx, st, [&] {
-               return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st);
-           }));
-    HIPCHK(h, timed(h, "census", npx, st, [&] {
-               return sgm::launch_census(d_right, pitch, g, h->p.blur, h->d_ct[1], st);
+    HIPCHK(h, timed(h, "census", 2 * npx, st, [&] {  // both images, one launch
+               return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st, false,
+                                         d_right, h->d_ct[1]);
            }));
     HIPCHK(h, hipEventRecord(h->ev_ct, st));
     if (h->nviews == 2) {

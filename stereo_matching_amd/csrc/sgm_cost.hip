@@ -52,10 +52,16 @@ constexpr int CT_TW = 64, CT_TH = 8;
 // CT_pts (cost.cpp:99-129) for one image; window (7/s) x (9/s), MSB first,
 // centre skipped, coordinates clamped to the (working-grid) edge.  The
 // (blurred) window is staged in LDS at clamped coordinates.
+// Both images in one launch: workgroup z selects (src0, ct0) or (src1, ct1).
 template <int HH, int HWW>
-__global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__ src, int rpitch,
+__global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__ src0,
+                                                     const uint8_t *__restrict__ src1, int rpitch,
                                                      int step, int H, int W, int blur,
-                                                     uint64_t *__restrict__ ct) {
+                                                     uint64_t *__restrict__ ct0,
+                                                     uint64_t *__restrict__ ct1) {
+    const bool second = __builtin_amdgcn_workgroup_id_z() != 0;
+    const uint8_t *__restrict__ src = second ? src1 : src0;
+    uint64_t *__restrict__ ct = second ? ct1 : ct0;
     constexpr int TR = CT_TH + 2 * HH, TC = CT_TW + 2 * HWW;
     __shared__ uint8_t tile[TR][TC];
     const int x0 = bid_x() * CT_TW, y0 = bid_y() * CT_TH;
@@ -84,13 +90,13 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
 }
 
 hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64_t *ct,
-                         hipStream_t st, bool bm_rows) {
-    dim3 grid((g.W + CT_TW - 1) / CT_TW, (g.H + CT_TH - 1) / CT_TH);
+                         hipStream_t st, bool bm_rows, const uint8_t *src2, uint64_t *ct2) {
+    dim3 grid((g.W + CT_TW - 1) / CT_TW, (g.H + CT_TH - 1) / CT_TH, src2 ? 2 : 1);
     const int rpitch = bm_rows ? pitch : pitch * g.scale;
     if (g.scale == 1)
-        census_kernel<3, 4><<<grid, 256, 0, st>>>(src, rpitch, 1, g.H, g.W, blur, ct);
+        census_kernel<3, 4><<<grid, 256, 0, st>>>(src, src2, rpitch, 1, g.H, g.W, blur, ct, ct2);
     else
-        census_kernel<1, 2><<<grid, 256, 0, st>>>(src, rpitch, 2, g.H, g.W, blur, ct);
+        census_kernel<1, 2><<<grid, 256, 0, st>>>(src, src2, rpitch, 2, g.H, g.W, blur, ct, ct2);
     return hipGetLastError();
 }
 

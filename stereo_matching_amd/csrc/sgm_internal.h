@@ -78,9 +78,11 @@ hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArg
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st);
 hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st);
 
-// bm_rows: BM.cpp:24-25 decimation (rows not strided by the scale)
+// bm_rows: BM.cpp:24-25 decimation (rows not strided by the scale); src2/ct2:
+// a second image censused in the same launch
 hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64_t *ct,
-                         hipStream_t st, bool bm_rows = false);
+                         hipStream_t st, bool bm_rows = false, const uint8_t *src2 = nullptr,
+                         uint64_t *ct2 = nullptr);
 // BM's WTA (BM.cpp:53-85) over the filtered cost: raw disparity + its float copy
 hipError_t launch_bm_wta(const float *cost, float uniq, uint16_t *disp, float *out, int out_pitch,
                          Geom g, hipStream_t st);
