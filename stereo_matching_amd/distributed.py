@@ -57,3 +57,48 @@ def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], gr
         h, w = compute(pairs[0]).shape  # shape only; no rank holds zero pairs when n >= world
         local = torch.empty((0, h, w))
     return gather_maps(local, len(pairs), group)
+
+
+class PipelinedGather:
+    """Per-step gather of a rank's map to rank 0, overlapped with the next
+    steps' compute.  Steps write into `buffer()` (one of `depth` rotating
+    maps), then call `submit()`, which enqueues an asynchronous gather of that
+    map (RCCL over xGMI: its stream waits for the map's producer, nothing
+    waits for it); a buffer's previous gather is only waited for when the
+    buffer comes round again, and `drain()` waits for all of them.  With
+    depth 2 the gather of step k runs under the kernels of step k+1."""
+
+    def __init__(self, shape, dtype, device, depth: int = 2, group=None):
+        self.group = group
+        self.depth = depth
+        world = dist.get_world_size(group)
+        self.root = dist.get_rank(group) == 0
+        self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(depth)]
+        self.recv = [[torch.empty(shape, dtype=dtype, device=device) for _ in range(world)]
+                     if self.root else None for _ in range(depth)]
+        self.work = [None] * depth
+        self.k = 0
+
+    def buffer(self) -> torch.Tensor:
+        i = self.k % self.depth
+        if self.work[i] is not None:
+            self.work[i].wait()
+            self.work[i] = None
+        return self.bufs[i]
+
+    def submit(self) -> None:
+        i = self.k % self.depth
+        self.work[i] = dist.gather(self.bufs[i], gather_list=self.recv[i], dst=0, group=self.group,
+                                   async_op=True)
+        self.k += 1
+
+    def drain(self) -> None:
+        for i, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[i] = None
+
+    def gathered(self, step: int):
+        """Rank 0: the maps of `step` (valid after drain() and while fewer than
+        `depth` later steps have been submitted); None elsewhere."""
+        return None if not self.root else self.recv[step % self.depth]

@@ -69,3 +69,43 @@ def test_gather_world2_gloo():
     want = np.stack([_compute(p).numpy() for p in _pairs()])
     assert res[0].shape == (N, H, W)
     assert np.array_equal(res[0].view(np.uint32), want.view(np.uint32))
+
+
+def _pipe_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pipe = distributed.PipelinedGather((3, 4), torch.float32, "cpu", depth=2)
+        seen = {}
+        for k in range(5):
+            buf = pipe.buffer()            # waits for the gather of step k-2
+            if k >= 2 and rank == 0:       # step k-2's maps are complete now
+                seen[k - 2] = [t.clone().numpy() for t in pipe.gathered(k - 2)]
+            buf.fill_(100 * rank + k)      # "compute" step k into the buffer
+            pipe.submit()
+        pipe.drain()
+        if rank == 0:
+            for k in (3, 4):
+                seen[k] = [t.clone().numpy() for t in pipe.gathered(k)]
+        q.put((rank, seen))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_gather_world2_gloo():
+    # bench.py's overlapped per-step gather: every step's maps reach rank 0
+    # intact although the next step already writes the other buffer
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(res[0]) == [0, 1, 2, 3, 4]
+    for k, maps in res[0].items():
+        for r in range(2):
+            assert (maps[r] == 100 * r + k).all(), (k, r)
