@@ -10,7 +10,9 @@ import os
 import subprocess
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libsgm_hip.so")
+# SGM_HIP_LIB points the loader at another build of the same library (the
+# instrumented -DSGM_STAMPS build of tools/stamps.py); default: the in-tree one
+LIB_PATH = os.environ.get("SGM_HIP_LIB") or os.path.join(_PKG, "libsgm_hip.so")
 CSRC = os.path.join(_PKG, "csrc")
 
 SGM_OK = 0

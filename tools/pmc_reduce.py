@@ -18,7 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = [("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
          ("pair_final_kernel", "pair_bwd_L4_final"), ("vfwd_kernel", "vfwd"),
          ("cost_h_kernel", "cost_h"), ("cost_h_global_kernel", "cost_h"),
-         ("census_kernel", "census"), ("lr_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc")]
+         ("census_kernel", "census"), ("lr_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc"),
+         ("median_fill_kernel", "post_median"), ("cc_local_kernel", "post_cc_local"),
+         ("cc_merge_kernel", "post_cc_merge"), ("cc_count_kernel", "post_cc_count"),
+         ("cc_apply_kernel", "post_cc_apply"), ("pf_prep_kernel", "post_prep"),
+         ("lk_refine_kernel", "lk_refine"), ("sky_columns_kernel", "sky_columns"),
+         ("sky_gray_kernel", "sky_gray"), ("bm_wta_kernel", "bm_wta")]
 
 
 def short(name):
