@@ -325,12 +325,13 @@ __global__ __launch_bounds__(256) void sky_mask_kernel(SkyViews sv, int H, int W
 
 size_t sky_scratch_bytes(Geom g) {
     const size_t W = (size_t)g.W, npx = (size_t)g.H * g.W;
-    return kSkyTotBytes                          // totals
-           + 4 * kSkyT * W                       // borders per threshold
-           + 3 * 4 * kSkyT * W                   // sky moments per threshold
-           + 2 * 4 * W                           // dark rows, final border
-           + npx                                 // gray image
-           + 64 + 24 * (size_t)((g.W + 63) / 64) * ((g.H + 15) / 16);  // gray partials
+    const size_t bytes = kSkyTotBytes            // totals
+                         + 4 * kSkyT * W         // borders per threshold
+                         + 3 * 4 * kSkyT * W     // sky moments per threshold
+                         + 2 * 4 * W             // dark rows, final border
+                         + npx                   // gray image
+                         + 64 + 24 * (size_t)((g.W + 63) / 64) * ((g.H + 15) / 16);  // partials
+    return (bytes + 255) & ~(size_t)255;  // the second view's scratch starts here: keep it aligned
 }
 
 hipError_t launch_sky_detect(const uint8_t *const *img, int pitch, uint8_t *const *mask,

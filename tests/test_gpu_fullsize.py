@@ -64,3 +64,43 @@ def test_4k256_properties():
     est = raw1[rows][:, D + 8: w - 8].astype(np.int64)
     hit = np.mean(np.abs(est - g[rows][:, None]) <= 1)
     assert hit > 0.9, hit
+
+
+def test_k128_full_pipeline_vs_oracle():
+    # node.cpp:80-107 at config 2's size: sky detector on both views, SGM,
+    # LR check, post_filter, then LKRefine (SGM.cpp:821-824), all on the GPU,
+    # against the oracle run stage by stage on the same inputs
+    h, w, D = 375, 1242, 128
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=2)
+    # a bright, smooth sky band so the detector has something to find
+    yy, xx = np.mgrid[0:h, 0:w]
+    band = yy < (40 + 25 * np.sin(xx / 90.0)).astype(int)
+    left = np.where(band, 200 + (yy // 9) % 2, left).astype(np.uint8)
+    right = np.where(band, 200 + (yy // 9) % 2, right).astype(np.uint8)
+    ml, mr = oracle.sky_detect(left), oracle.sky_detect(right)
+    assert (ml == 255).any()
+    ref = oracle.process(left, right, D, sky_l=ml, sky_r=mr)
+    want = oracle.lk_refine(left, right, ref["final"], D)
+    with SGM(h, w, 1, D, post_filter=True, lk_refine=True, sky_detect=True) as sgm:
+        sgm.process(left, right)
+        got = sgm.get_disp().copy()
+    mism = int(np.count_nonzero(_bits(got) != _bits(want)))
+    assert mism == 0, f"{mism} mismatching pixels"
+
+
+def test_4k256_side_stages_vs_oracle():
+    # config 5's frame: the SGM map comes from the GPU (the oracle's 4K SGM
+    # needs ~76 GB); post_filter, LKRefine and the sky detector are checked
+    # bit for bit against the oracle on that map and those images
+    h, w, D = 2160, 3840, 256
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=3)
+    with SGM(h, w, 1, D, views=2) as sgm:
+        sgm.process(left, right)
+        lr = sgm.get_lr_disp().copy()
+        post = sgm.post_filter(lr)
+        lk = sgm.lk_refine(left, right, post)
+        sky = sgm.sky_detect(left)
+    want_post = oracle.post_filter(lr, D)
+    assert np.array_equal(_bits(post), _bits(want_post))
+    assert np.array_equal(_bits(lk), _bits(oracle.lk_refine(left, right, want_post, D)))
+    assert np.array_equal(sky, oracle.sky_detect(left))

@@ -56,3 +56,19 @@ def test_process_with_sky_detect():
         sgm.process(left, right)
         got = sgm.get_lr_disp()
     assert np.array_equal(got.view(np.uint32), ref["lr"].view(np.uint32))
+
+
+@pytest.mark.parametrize("hw", [(96, 300), (375, 1242), (61, 203)])
+def test_process_with_sky_detect_odd_sizes(hw):
+    # both views' detections share one launch sequence with per-view scratch;
+    # H*W not a multiple of 8 once misaligned the second view's totals
+    h, w = hw
+    D = 64
+    left = sky_images.make("horizon", h, w, seed=7)
+    right = np.roll(left, -5, axis=1)
+    ml, mr = oracle.sky_detect(left), oracle.sky_detect(right)
+    ref = oracle.process(left, right, D, sky_l=ml, sky_r=mr)
+    with SGM(h, w, 1, D, device=0, sky_detect=True) as sgm:
+        sgm.process(left, right)
+        got = sgm.get_lr_disp()
+    assert np.array_equal(got.view(np.uint32), ref["lr"].view(np.uint32))
