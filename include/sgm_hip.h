@@ -77,7 +77,8 @@ typedef struct sgm_params {
                           at SGM.cpp:824 is commented out in the reference); 0 (default) */
     int sky_detect;    /* 1: the sky masks of both views come from SkyAreaDetector::detect
                           run on the GPU over the input images (node.cpp:80-93), replacing
-                          any masks passed in; 0 (default): masks as passed (or none) */
+                          any masks passed in; 0 (default): masks as passed (or none).
+                          Working grid up to 8192 columns and 4784 rows */
     int solver;        /* SGM_SOLVER_SGM (default) or SGM_SOLVER_BM.  BM: out = the raw
                           WTA disparity as float (BM.cpp:53-85; post_filter()ed when
                           post_filter is set, BM.cpp:88), raw_disp = the same as u16;

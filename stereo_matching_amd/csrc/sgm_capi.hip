@@ -121,6 +121,12 @@ bool valid_params(const sgm_params *p, char *why, size_t n) {
     const int H = p->height / p->scale, W = p->width / p->scale;
     if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
     if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
+    // the sky detector keeps a row of borders (W <= 8192) and the top half of a
+    // 64-column strip (H/2 + 2 rows of 68 B <= ~159 KiB) in LDS (sgm_sky.hip)
+    if (p->sky_detect && (W > 8192 || (size_t)(H / 2 + 2) * 68 > 160 * 1024 - 1024)) {
+        snprintf(why, n, "sky_detect supports working grids up to 8192 x %d", 2 * ((160 * 1024 - 1024) / 68 - 2));
+        return false;
+    }
     if (p->solver != SGM_SOLVER_SGM && p->solver != SGM_SOLVER_BM) {
         snprintf(why, n, "solver must be SGM_SOLVER_SGM or SGM_SOLVER_BM");
         return false;

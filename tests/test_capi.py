@@ -67,6 +67,31 @@ def test_invalid_arguments_rejected(lib, h, w, s, d):
     assert not handle.value
 
 
+@pytest.mark.parametrize("field,value,h,w", [("solver", 7, 375, 1242), ("sky_detect", 1, 100, 9000),
+                                             ("sky_detect", 1, 5000, 100), ("views", 3, 375, 1242)])
+def test_invalid_stage_parameters_rejected(lib, field, value, h, w):
+    # parameters of the section-8f stages are checked at sgm_create, before
+    # any device work (sky detector limits: sgm_sky.hip)
+    p = _capi.Params()
+    lib.sgm_default_params(ctypes.byref(p), h, w, 1, 64)
+    setattr(p, field, value)
+    handle = ctypes.c_void_p()
+    assert lib.sgm_create(ctypes.byref(p), 0, ctypes.byref(handle)) == _capi.SGM_ERR_INVALID_ARG
+    assert not handle.value
+
+
+def test_stage_entry_points_reject_null(lib):
+    for fn, nargs in (("sgm_post_filter_device", 4), ("sgm_lk_refine_device", 7),
+                      ("sgm_sky_detect_device", 6), ("sgm_colormap_device", 6),
+                      ("sgm_point_cloud_device", 10), ("sgm_stage_post_filter", 2),
+                      ("sgm_stage_lk_refine", 5), ("sgm_stage_sky_detect", 4),
+                      ("sgm_stage_colormap", 3), ("sgm_stage_point_cloud", 8)):
+        f = getattr(lib, fn)
+        assert len(f.argtypes) == nargs, fn
+        args = [0 if t is ctypes.c_int else None for t in f.argtypes]
+        assert f(*args) == _capi.SGM_ERR_INVALID_ARG, fn
+
+
 def test_null_arguments_rejected(lib):
     assert lib.sgm_create(None, 0, None) == _capi.SGM_ERR_INVALID_ARG
     assert lib.sgm_destroy(None) == _capi.SGM_ERR_INVALID_ARG
