@@ -34,20 +34,152 @@ constexpr int kLW = kMW + 4;   // LDS row: two halo columns each side
 constexpr int kNoSample = 0x7fff;  // encodes an invalid sample (above any disparity)
 constexpr int kSnapN = 2 * kMW + 8 + 4 * kMH;  // working-map cells a tile reads (200)
 
-// k-th smallest (0-based) of the samples: the largest t with #(v < t) <= k,
-// built bit by bit (disparities are < 256).  Invalid samples never count.
-template <int N>
-__device__ __forceinline__ int kth_smallest(const int (&v)[N], int extra0, int extra1, int k) {
-    int res = 0;
-#pragma unroll
-    for (int b = 7; b >= 0; --b) {
-        const int t = res | (1 << b);
-        int c = (extra0 < t) + (extra1 < t);
-#pragma unroll
-        for (int q = 0; q < N; ++q) c += v[q] < t;
-        if (c <= k) res = t;
+// Batcher's odd-even merge sort for 32 inputs, pruned to 22 (a comparator
+// touching a +inf pad is a no-op): 119 compare-exchanges, checked on all
+// 2^22 0/1 inputs (0-1 principle).
+__device__ __forceinline__ void sort22(int (&f)[22]) {
+#define CE(i, j)                              \
+    {                                         \
+        const int a_ = f[i], b_ = f[j];       \
+        f[i] = a_ < b_ ? a_ : b_;             \
+        f[j] = a_ < b_ ? b_ : a_;             \
     }
-    return res;
+    CE(0, 1);
+    CE(2, 3);
+    CE(0, 2);
+    CE(1, 3);
+    CE(1, 2);
+    CE(4, 5);
+    CE(6, 7);
+    CE(4, 6);
+    CE(5, 7);
+    CE(5, 6);
+    CE(0, 4);
+    CE(2, 6);
+    CE(2, 4);
+    CE(1, 5);
+    CE(3, 7);
+    CE(3, 5);
+    CE(1, 2);
+    CE(3, 4);
+    CE(5, 6);
+    CE(8, 9);
+    CE(10, 11);
+    CE(8, 10);
+    CE(9, 11);
+    CE(9, 10);
+    CE(12, 13);
+    CE(14, 15);
+    CE(12, 14);
+    CE(13, 15);
+    CE(13, 14);
+    CE(8, 12);
+    CE(10, 14);
+    CE(10, 12);
+    CE(9, 13);
+    CE(11, 15);
+    CE(11, 13);
+    CE(9, 10);
+    CE(11, 12);
+    CE(13, 14);
+    CE(0, 8);
+    CE(4, 12);
+    CE(4, 8);
+    CE(2, 10);
+    CE(6, 14);
+    CE(6, 10);
+    CE(2, 4);
+    CE(6, 8);
+    CE(10, 12);
+    CE(1, 9);
+    CE(5, 13);
+    CE(5, 9);
+    CE(3, 11);
+    CE(7, 15);
+    CE(7, 11);
+    CE(3, 5);
+    CE(7, 9);
+    CE(11, 13);
+    CE(1, 2);
+    CE(3, 4);
+    CE(5, 6);
+    CE(7, 8);
+    CE(9, 10);
+    CE(11, 12);
+    CE(13, 14);
+    CE(16, 17);
+    CE(18, 19);
+    CE(16, 18);
+    CE(17, 19);
+    CE(17, 18);
+    CE(20, 21);
+    CE(16, 20);
+    CE(18, 20);
+    CE(17, 21);
+    CE(19, 21);
+    CE(17, 18);
+    CE(19, 20);
+    CE(18, 20);
+    CE(19, 21);
+    CE(17, 18);
+    CE(19, 20);
+    CE(0, 16);
+    CE(8, 16);
+    CE(4, 20);
+    CE(12, 20);
+    CE(4, 8);
+    CE(12, 16);
+    CE(2, 18);
+    CE(10, 18);
+    CE(6, 10);
+    CE(14, 18);
+    CE(2, 4);
+    CE(6, 8);
+    CE(10, 12);
+    CE(14, 16);
+    CE(18, 20);
+    CE(1, 17);
+    CE(9, 17);
+    CE(5, 21);
+    CE(13, 21);
+    CE(5, 9);
+    CE(13, 17);
+    CE(3, 19);
+    CE(11, 19);
+    CE(7, 11);
+    CE(15, 19);
+    CE(3, 5);
+    CE(7, 9);
+    CE(11, 13);
+    CE(15, 17);
+    CE(19, 21);
+    CE(1, 2);
+    CE(3, 4);
+    CE(5, 6);
+    CE(7, 8);
+    CE(9, 10);
+    CE(11, 12);
+    CE(13, 14);
+    CE(15, 16);
+    CE(17, 18);
+    CE(19, 20);
+#undef CE
+}
+
+// k-th smallest (0-based) of the sorted fixed samples f and two more, a <= b:
+// the merged order is f[0..ra), a, f[ra..rb), b, f[rb..) with ra = #(f < a),
+// rb = #(f < b).  Invalid samples (kNoSample) sort last; k < #valid, so the
+// answer is always a valid sample.  sf: this lane's column of the sorted
+// samples in LDS (sf[q * 64] = f[q]), read at the three candidate ranks.
+__device__ __forceinline__ int kth_merged(const int (&f)[22], const int *sf, int a, int b, int k) {
+    int ra = 0, rb = 0;
+#pragma unroll
+    for (int q = 0; q < 22; ++q) {
+        ra += f[q] < a;
+        rb += f[q] < b;
+    }
+    const int x0 = sf[k * 64], x1 = sf[(k - 1) * 64], x2 = sf[(k - 2) * 64];
+    return k < ra ? x0 : (k == ra ? a : (k <= rb ? x1 : (k == rb + 1 ? b : x2)));
 }
 
 // std::vector<int> v.push_back(float) truncates (Solver.cpp:605,619)
@@ -67,13 +199,14 @@ __global__ __launch_bounds__(64) void median_fill_kernel(const float *__restrict
     __shared__ float O[kMH + 4][kLW];   // window grid (rows r0-2 .. r0+kMH+1)
     __shared__ float FL[kMH][2], FR[kMH][2];  // working-map halo columns of the tile rows
     __shared__ float FC[kMH][kMW];            // the working map's tile cells (change test)
+    __shared__ int SF[22][kMW];               // each lane's sorted fixed samples of the row
     if (iter > 0 && changes[iter - 1] == 0) return;  // the last launch proved the fixed point
     const int tx = bid_x(), ty = bid_y(), ntx = (int)gridDim.x;
     const int tile = ty * ntx + tx;
     const int lane = tid_x();
     const int r0 = ty * kMH, c0 = tx * kMW;
     const float out = dmax + 2.f;  // outside the frame: never a sample of an interior window
-    auto at = [&](const float *m, int i, int j) {  // branch-free clamped load
+    auto at = [=](const float *m, int i, int j) {  // branch-free clamped load
         const float v = m[(size_t)clampi(i, 0, H - 1) * W + clampi(j, 0, W - 1)];
         return (i >= 0 && i < H && j >= 0 && j < W) ? v : out;
     };
@@ -144,6 +277,13 @@ __global__ __launch_bounds__(64) void median_fill_kernel(const float *__restrict
             int nfixed = 0;
 #pragma unroll
             for (int q = 0; q < 22; ++q) nfixed += fixed[q] != kNoSample;
+            // a fill needs more than 12 samples: with at most 2 chained ones,
+            // lanes with <= 10 fixed samples can never fill
+            if (__ballot(active && nfixed > 10)) {
+                sort22(fixed);
+#pragma unroll
+                for (int q = 0; q < 22; ++q) SF[q][lane] = fixed[q];
+            }
             // the in-row chain: iterate the row to its fixed point
             for (int it = 0; it <= kMW; ++it) {
                 const float u1 = shfl_up(cur, 1), u2 = shfl_up(cur, 2);
@@ -152,7 +292,9 @@ __global__ __launch_bounds__(64) void median_fill_kernel(const float *__restrict
                 const int s1 = sample(l1, dmax), s2 = sample(l2, dmax);
                 const int cnt = nfixed + (s1 != kNoSample) + (s2 != kNoSample);
                 float nv = own;
-                if (active && cnt > 12) nv = (float)kth_smallest(fixed, s1, s2, cnt / 2);
+                if (active && cnt > 12)
+                    nv = (float)kth_merged(fixed, &SF[0][lane], s1 < s2 ? s1 : s2,
+                                           s1 < s2 ? s2 : s1, cnt / 2);
                 const bool diff = __float_as_uint(nv) != __float_as_uint(cur);
                 cur = nv;
                 if (!__ballot(diff)) break;
