@@ -116,6 +116,10 @@ def parse():
                     help="end each step with LKRefine on the GPU (SGM.cpp:824, LKSubPixelImpl.cpp)")
     ap.add_argument("--sky-detect", action="store_true",
                     help="start each step with the sky detector on both views (node.cpp:80-93)")
+    ap.add_argument("--view-split", action="store_true",
+                    help="N even, V=2 configs: one pair per two GPUs, left view on the even rank, "
+                         "right view on the odd one, F_R over RCCL point-to-point (SURVEY.md 8e "
+                         "optional split; a latency option, not the default sharding)")
     ap.add_argument("--host-io", action="store_true",
                     help="also time sgm_process on host buffers (PCIe-inclusive, not `value`)")
     return ap.parse_args()
@@ -138,28 +142,41 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.view_split and (world % 2 or views != 2):
+        raise SystemExit("--view-split needs an even number of ranks and a two-view config")
 
     from stereo_matching_amd import SGM, synthetic
 
-    # one synthetic pair per rank (weak scaling: per-GPU work is fixed)
-    left, right = synthetic.stereo_pair(h, w, D, pair_index=rank)
+    # one synthetic pair per rank (weak scaling: per-GPU work is fixed); with
+    # --view-split one pair per two ranks
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=rank // 2 if args.view_split else rank)
     d_left = torch.from_numpy(left).to(dev)
     d_right = torch.from_numpy(right).to(dev)
     d_out = torch.empty((h, w), dtype=torch.float32, device=dev)
     # N > 1: each step's map goes to rank 0 by a gather that overlaps the next
     # step's kernels (double-buffered maps, stereo_matching_amd.distributed)
     pipe = None
-    if world > 1:
+    if world > 1 and not args.view_split:
         from stereo_matching_amd.distributed import PipelinedGather
         pipe = PipelinedGather((h, w), torch.float32, dev, depth=2)
 
     if cfg.get("full"):
         args.post_filter = args.lk_refine = args.sky_detect = True
-    sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter,
-              lk_refine=args.lk_refine, sky_detect=args.sky_detect)
+    team = None
+    if args.view_split:
+        from stereo_matching_amd.distributed import ViewSplit
+        sgm = SGM(h, w, 1, D, views=1, view="right" if rank % 2 else "left", device=local,
+                  sky_detect=args.sky_detect)
+        team = ViewSplit(sgm, h, w, dev, post_filter=args.post_filter, lk_refine=args.lk_refine)
+    else:
+        sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter,
+                  lk_refine=args.lk_refine, sky_detect=args.sky_detect)
     stream = torch.cuda.current_stream(dev)
 
     def step():
+        if team:
+            team.step(d_left.data_ptr(), d_right.data_ptr(), d_out)
+            return
         out = pipe.buffer() if pipe else d_out
         sgm.process_device(d_left.data_ptr(), d_right.data_ptr(), out.data_ptr(),
                            stream=stream.cuda_stream)
@@ -192,7 +209,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    units = float(world) * views * h * w * D * args.steps
+    pairs = world // 2 if args.view_split else world
+    units = float(pairs) * views * h * w * D * args.steps
     value = units / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -301,9 +319,13 @@ def main():
                        + (" + LKRefine" if args.lk_refine else ""),
                        "width": w, "height": h, "max_disp": D, "views": views,
                        "post_filter": bool(args.post_filter), "lk_refine": bool(args.lk_refine),
-                       "sky_detect": bool(args.sky_detect), "pairs_per_gpu": 1, "global_batch": world,
-                       "parallelism": f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0 "
-                                      f"overlapped with the next step"},
+                       "sky_detect": bool(args.sky_detect),
+                       "pairs_per_gpu": 0.5 if args.view_split else 1, "global_batch": pairs,
+                       "parallelism": (f"view-split x{pairs} (left/right view per GPU, F_R over "
+                                       f"RCCL point-to-point; maps stay on the even ranks)"
+                                       if args.view_split else
+                                       f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0 "
+                                       f"overlapped with the next step")},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
             "host_io": host_io,
         }

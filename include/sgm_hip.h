@@ -86,7 +86,17 @@ typedef struct sgm_params {
     int aux_only;      /* 1: a light handle for the per-frame side stages only (sky detector,
                           post_filter, LKRefine, colormap, point cloud): no cost volumes are
                           allocated and sgm_process[_device] refuse; 0 (default) */
+    int view;          /* with views == 1: SGM_VIEW_LEFT (default), the left view
+                          (SGM.cpp:32-445, disp/filtered_disp); or SGM_VIEW_RIGHT, the right
+                          view alone (SGM.cpp:448-801: build_dsi_from_table_beta, the same
+                          8 paths, disp_beta/filtered_disp_beta), so that a pair's two views
+                          can run on two GPUs and meet in sgm_lr_check_device.
+                          A right-view handle has no post_filter/lk_refine (they follow the
+                          LR check on the left view's GPU) and uses sky_r (or the right image's
+                          detected mask) */
 } sgm_params;
+
+enum { SGM_VIEW_LEFT = 0, SGM_VIEW_RIGHT = 1 };
 
 /* Camera of the point cloud (CamIntrinsics, inc/utils.h:14-20, plus the two
  * constants of node.cpp:122-123). */
@@ -121,8 +131,10 @@ size_t sgm_device_bytes(const sgm_handle *h);
  *                (filtered_disp after SGM.cpp:818), invalid = D+1; with
  *                params.post_filter it is then post_filter()ed on the GPU
  *                (SGM.cpp:821, what get_disp() returns); with views == 1 it
- *                is the left sub-pixel map (SGM.cpp:443)
- *   raw_disp   : optional u16 rows x cols, left WTA disparity (SGM.cpp:411-415)
+ *                is the left sub-pixel map (SGM.cpp:443), or the right one
+ *                (filtered_disp_beta, SGM.cpp:801) with params.view == SGM_VIEW_RIGHT
+ *   raw_disp   : optional u16 rows x cols, left WTA disparity (SGM.cpp:411-415;
+ *                disp_beta, SGM.cpp:755-795, with SGM_VIEW_RIGHT)
  */
 int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
                 const uint8_t *sky_l, const uint8_t *sky_r, int sky_pitch,
@@ -135,6 +147,17 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
                        float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream);
+
+/* The LR check of SGM.cpp:803-818 on DEVICE working-grid maps: out(i, j) =
+ * fl(i, j), or D+1 where j >= fl and |fl - fr(i, (int)(j - fl/s))| > lr_max_diff.
+ * fl is the left view's sub-pixel map (filtered_disp), fr the right view's
+ * (filtered_disp_beta), e.g. from two SGM_VIEW_LEFT / SGM_VIEW_RIGHT handles on
+ * two GPUs with fr copied over; pitches in floats; d_out may alias d_fl but not
+ * d_fr.  Any handle of the working size (aux_only included) serves.  Enqueued
+ * on `stream` (NULL = the handle's stream); sgm_post_filter_device and
+ * sgm_lk_refine_device then complete get_disp()'s map. */
+int sgm_lr_check_device(sgm_handle *h, const float *d_fl, int fl_pitch, const float *d_fr,
+                        int fr_pitch, float *d_out, int out_pitch, void *stream);
 
 /* post_filter() (Solver.cpp:600-649) on a host rows x cols f32 map, in place:
  * 5x5 median fill + speckle removal, single-thread semantics, on the host CPU

@@ -22,6 +22,8 @@ SGM_ERR_HIP = 3
 SGM_ERR_NO_DEVICE = 4
 SGM_SOLVER_SGM = 0
 SGM_SOLVER_BM = 1
+SGM_VIEW_LEFT = 0
+SGM_VIEW_RIGHT = 1
 
 # Every symbol include/sgm_hip.h declares.
 EXPORTS = (
@@ -31,7 +33,7 @@ EXPORTS = (
     "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
     "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine", "sgm_sky_detect_device",
     "sgm_stage_sky_detect", "sgm_colormap_device", "sgm_point_cloud_device", "sgm_stage_colormap",
-    "sgm_stage_point_cloud",
+    "sgm_stage_point_cloud", "sgm_lr_check_device",
 )
 
 
@@ -49,6 +51,7 @@ class Params(ctypes.Structure):
         ("blur", ctypes.c_int), ("views", ctypes.c_int), ("post_filter", ctypes.c_int),
         ("lk_refine", ctypes.c_int), ("sky_detect", ctypes.c_int),
         ("solver", ctypes.c_int), ("aux_only", ctypes.c_int),
+        ("view", ctypes.c_int),
     ]
 
 
@@ -99,6 +102,7 @@ def lib():
     L.sgm_process_device.argtypes = [P, P, P, I, P, P, I, P, I, P, P]
     L.sgm_post_filter_host.argtypes = [P, I, I, I, I]
     L.sgm_post_filter_device.argtypes = [P, P, I, P]
+    L.sgm_lr_check_device.argtypes = [P, P, I, P, I, P, I, P]
     L.sgm_stage_post_filter.argtypes = [P, P]
     L.sgm_lk_refine_device.argtypes = [P, P, P, I, P, I, P]
     L.sgm_stage_lk_refine.argtypes = [P, P, P, I, P]

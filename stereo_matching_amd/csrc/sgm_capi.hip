@@ -121,6 +121,15 @@ bool valid_params(const sgm_params *p, char *why, size_t n) {
     const int H = p->height / p->scale, W = p->width / p->scale;
     if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
     if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
+    if (p->view != SGM_VIEW_LEFT && p->view != SGM_VIEW_RIGHT) {
+        snprintf(why, n, "view must be SGM_VIEW_LEFT or SGM_VIEW_RIGHT");
+        return false;
+    }
+    if (p->view == SGM_VIEW_RIGHT &&
+        (p->views != 1 || p->solver != SGM_SOLVER_SGM || p->post_filter || p->lk_refine)) {
+        snprintf(why, n, "SGM_VIEW_RIGHT needs views == 1, the SGM solver and no post_filter/lk_refine");
+        return false;
+    }
     // the sky detector keeps a row of borders (W <= 8192) and the top half of a
     // 64-column strip (H/2 + 2 rows of 68 B <= ~159 KiB) in LDS (sgm_sky.hip)
     if (p->sky_detect && (W > 8192 || (size_t)(H / 2 + 2) * 68 > 160 * 1024 - 1024)) {
@@ -303,12 +312,13 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     return SGM_OK;
 }
 
-// build_dsi_from_table[_beta] + horizontal IIR (cost_h), then the vertical IIR
-// fused with the L3 forward pass (vfwd).
-int cost_view(sgm_handle *h, int view, const uint8_t *sky, int sky_pitch, hipStream_t st) {
+// build_dsi_from_table[_beta] (dsi 0 / 1) + horizontal IIR (cost_h), then
+// the vertical IIR fused with the L3 forward pass (vfwd), into view slot
+// `view`'s buffers.
+int cost_view(sgm_handle *h, int view, int dsi, const uint8_t *sky, int sky_pitch, hipStream_t st) {
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     HIPCHK(h, timed(h, "cost_h", elems, st, [&] {
-               return sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky, sky_pitch, view, 1, h->g,
+               return sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky, sky_pitch, dsi, 1, h->g,
                                          h->d_ch[view], st);
            }));
     sgm::PairArgs pa = pair_args(h);
@@ -344,7 +354,7 @@ int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int p
                                          h->d_ct[1]);
            }));
     int rc;
-    if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
+    if ((rc = cost_view(h, 0, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
     HIPCHK(h, timed(h, "bm_wta", elems, st, [&] {
                return sgm::launch_bm_wta(h->d_c[0], h->p.uniqueness, h->d_disp[0], d_out, out_pitch,
                                          g, st);
@@ -370,14 +380,16 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         return bm_frame(h, d_left, d_right, pitch, d_sky_l, sky_pitch, d_out, out_pitch, d_raw, st);
     hipStream_t aux1 = h->concurrent_views ? h->aux[0] : st;  // right view
     const double npx = (double)g.H * g.W;
+    // a right-view handle (SGM_VIEW_RIGHT) runs the right view in slot 0
+    const bool right_only = h->p.view == SGM_VIEW_RIGHT;
     if (h->p.sky_detect) {  // node.cpp:80-93: detect on both inputs, then process with the masks
-        const uint8_t *imgs[2] = {d_left, d_right};
+        const uint8_t *imgs[2] = {right_only ? d_right : d_left, d_right};
         HIPCHK(h, timed(h, "sky_detect", npx, st, [&] {
                    return sgm::launch_sky_detect(imgs, pitch, h->d_sky, g.W, h->d_sky_scratch,
                                                  h->nviews, g, st);
                }));
         d_sky_l = h->d_sky[0];
-        d_sky_r = h->nviews == 2 ? h->d_sky[1] : nullptr;
+        d_sky_r = right_only ? h->d_sky[0] : h->nviews == 2 ? h->d_sky[1] : nullptr;
         sky_pitch = g.W;
     }
     HIPCHK(h, timed(h, "census", 2 * npx, st, [&] {  // both images, one launch
@@ -387,10 +399,12 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     HIPCHK(h, hipEventRecord(h->ev_ct, st));
     if (h->nviews == 2) {
         HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
-        if ((rc = cost_view(h, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
+        if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
         HIPCHK(h, hipEventRecord(h->ev_c[1], aux1));
     }
-    if ((rc = cost_view(h, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
+    if ((rc = cost_view(h, 0, right_only ? 1 : 0, right_only ? d_sky_r : d_sky_l, sky_pitch, st)) !=
+        SGM_OK)
+        return rc;
     HIPCHK(h, hipEventRecord(h->ev_c[0], st));
     if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
                              false)) != SGM_OK)
@@ -402,7 +416,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
         HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
         HIPCHK(h, timed(h, "lr", npx, st, [&] {
-                   return sgm::launch_lr(h->d_sub[0], h->d_sub[1], d_out, out_pitch,
+                   return sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
                                          h->p.lr_max_diff, g, st);
                }));
     } else {
@@ -539,6 +553,7 @@ int sgm_default_params(sgm_params *p, int h, int w, int s, int d) {
     p->sky_detect = 0;       // 1: masks from SkyAreaDetector::detect on the GPU (node.cpp:80-93)
     p->solver = SGM_SOLVER_SGM;
     p->aux_only = 0;
+    p->view = SGM_VIEW_LEFT;
     return SGM_OK;
 }
 
@@ -873,6 +888,23 @@ int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float 
     return SGM_OK;
 }
 
+int sgm_lr_check_device(sgm_handle *h, const float *d_fl, int fl_pitch, const float *d_fr,
+                        int fr_pitch, float *d_out, int out_pitch, void *stream) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    const int W = h->g.W;
+    if (!d_fl || !d_fr || !d_out || fl_pitch < W || fr_pitch < W || out_pitch < W)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_lr_check_device: bad pointer or pitch");
+    if (d_out == d_fr)
+        return set_err(h, SGM_ERR_INVALID_ARG, "sgm_lr_check_device: d_out must not alias d_fr");
+    DeviceGuard guard(h->device);
+    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    HIPCHK(h, timed(h, "lr", (double)h->g.H * W, st, [&] {
+               return sgm::launch_lr(d_fl, fl_pitch, d_fr, fr_pitch, d_out, out_pitch,
+                                     h->p.lr_max_diff, h->g, st);
+           }));
+    return SGM_OK;
+}
+
 int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream) {
     if (!h) return SGM_ERR_INVALID_ARG;
     if (!d_disp || pitch < h->g.W)
@@ -1033,7 +1065,8 @@ int sgm_stage_lr(sgm_handle *h, const float *fl, const float *fr, float *out) {
     const size_t npx = (size_t)h->g.H * h->g.W;
     HIPCHK(h, hipMemcpyAsync(h->d_sub[0], fl, npx * 4, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, hipMemcpyAsync(h->d_sub[1], fr, npx * 4, hipMemcpyHostToDevice, h->st));
-    HIPCHK(h, sgm::launch_lr(h->d_sub[0], h->d_sub[1], h->d_out, h->g.W, h->p.lr_max_diff, h->g, h->st));
+    HIPCHK(h, sgm::launch_lr(h->d_sub[0], h->g.W, h->d_sub[1], h->g.W, h->d_out, h->g.W,
+                             h->p.lr_max_diff, h->g, h->st));
     HIPCHK(h, hipMemcpyAsync(out, h->d_out, npx * 4, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return SGM_OK;

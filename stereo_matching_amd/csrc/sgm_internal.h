@@ -119,7 +119,7 @@ hipError_t launch_point_cloud(const float *disp, int pitch, const uint8_t *img, 
                               float fx, float fy, float cx, float cy, double baseline,
                               float max_range, int *counts, double *xyz, uint8_t *pixel,
                               int *total, Geom g, hipStream_t st);
-hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
-                     Geom g, hipStream_t st);
+hipError_t launch_lr(const float *fl, int fl_pitch, const float *fr, int fr_pitch, float *out,
+                     int out_pitch, float lr, Geom g, hipStream_t st);
 
 }  // namespace sgm

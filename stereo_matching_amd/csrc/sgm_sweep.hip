@@ -70,26 +70,26 @@ hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream
 // ------------------------------------------------------------- LR check
 
 // SGM.cpp:803-818: dr = FR[i][(int)(j - dl/s)] when j >= dl; invalid if
-// |dl - dr| > LR_CHECK_DIS.
-__global__ __launch_bounds__(256) void lr_kernel(const float *__restrict__ fl,
-                                                 const float *__restrict__ fr,
-                                                 float *__restrict__ out, int out_pitch, int H,
-                                                 int W, int D, int scale, float lr) {
+// |dl - dr| > LR_CHECK_DIS.  Pitches in floats; out may alias fl.
+__global__ __launch_bounds__(256) void lr_kernel(const float *fl, int fl_pitch,
+                                                 const float *__restrict__ fr, int fr_pitch,
+                                                 float *out, int out_pitch, int H, int W, int D,
+                                                 int scale, float lr) {
     const int j = bid_x() * 256 + tid_x(), i = bid_y();
     if (j >= W) return;
-    float dl = fl[(size_t)i * W + j];
+    float dl = fl[(size_t)i * fl_pitch + j];
     if (j >= dl) {
         const int jr = clampi((int)(j - dl / scale), 0, W - 1);
-        const float dr = fr[(size_t)i * W + jr];
+        const float dr = fr[(size_t)i * fr_pitch + jr];
         if (fabsf(dl - dr) > lr) dl = (float)(D + 1);
     }
     out[(size_t)i * out_pitch + j] = dl;
 }
 
-hipError_t launch_lr(const float *fl, const float *fr, float *out, int out_pitch, float lr,
-                     Geom g, hipStream_t st) {
-    lr_kernel<<<dim3((g.W + 255) / 256, g.H), 256, 0, st>>>(fl, fr, out, out_pitch, g.H, g.W, g.D,
-                                                           g.scale, lr);
+hipError_t launch_lr(const float *fl, int fl_pitch, const float *fr, int fr_pitch, float *out,
+                     int out_pitch, float lr, Geom g, hipStream_t st) {
+    lr_kernel<<<dim3((g.W + 255) / 256, g.H), 256, 0, st>>>(fl, fl_pitch, fr, fr_pitch, out,
+                                                           out_pitch, g.H, g.W, g.D, g.scale, lr);
     return hipGetLastError();
 }
 

@@ -102,3 +102,67 @@ class PipelinedGather:
         """Rank 0: the maps of `step` (valid after drain() and while fewer than
         `depth` later steps have been submitted); None elsewhere."""
         return None if not self.root else self.recv[step % self.depth]
+
+
+class ViewSplit:
+    """One stereo pair over two GPUs (the optional
+    split): ranks 2k and 2k+1 of `group` form a team.  The even rank computes
+    the left view (SGM.cpp:32-445), the odd rank the right view (SGM.cpp:
+    448-801, an `SGM(..., views=1, view="right")` handle); the odd rank sends
+    its sub-pixel map F_R (rows x cols f32, 1.86 MB at K128) to the even rank
+    -- RCCL point-to-point over xGMI with backend "nccl", staged through host
+    memory with gloo -- and the even rank runs the LR check (SGM.cpp:803-818)
+    and, as asked, post_filter and LKRefine on the map.
+
+    `sgm` is this rank's handle (left view on even ranks, right view on odd
+    ones); `device` the torch device its maps live on.  Latency per pair is
+    one view plus the exchange instead of two views; throughput per GPU is
+    the same or lower, which is why pair sharding stays the default."""
+
+    def __init__(self, sgm, rows: int, cols: int, device, *, post_filter: bool = False,
+                 lk_refine: bool = False, group=None):
+        self.group = group
+        rank = dist.get_rank(group)
+        if dist.get_world_size(group) % 2:
+            raise ValueError("ViewSplit needs an even number of ranks")
+        self.role = rank % 2               # 0: left view + LR check, 1: right view
+        self.partner = rank ^ 1
+        self.partner_global = self.partner if group is None else \
+            dist.get_global_rank(group, self.partner)
+        self.sgm = sgm
+        self.device = torch.device(device)
+        self.post_filter, self.lk_refine = post_filter, lk_refine
+        self.fr = torch.empty((rows, cols), dtype=torch.float32, device=self.device)
+        self.staged = dist.get_backend(group) != "nccl" and self.device.type != "cpu"
+        self.host = torch.empty((rows, cols), dtype=torch.float32) if self.staged else None
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+
+    def step(self, d_left: int, d_right: int, out: torch.Tensor | None = None):
+        """Processes the team's pair (device images at the handle's full size);
+        on the even rank writes get_disp()'s map into `out` and returns it,
+        on the odd rank returns None."""
+        st = self._stream()
+        if self.role == 1:
+            self.sgm.process_device(d_left, d_right, self.fr.data_ptr(), stream=st)
+            if self.staged:
+                self.host.copy_(self.fr)
+                dist.send(self.host, dst=self.partner_global, group=self.group)
+            else:
+                dist.send(self.fr, dst=self.partner_global, group=self.group)
+            return None
+        if out is None:
+            out = torch.empty_like(self.fr)
+        self.sgm.process_device(d_left, d_right, out.data_ptr(), stream=st)
+        if self.staged:
+            dist.recv(self.host, src=self.partner_global, group=self.group)
+            self.fr.copy_(self.host)
+        else:
+            dist.recv(self.fr, src=self.partner_global, group=self.group)
+        self.sgm.lr_check_device(out.data_ptr(), self.fr.data_ptr(), out.data_ptr(), stream=st)
+        if self.post_filter:
+            self.sgm.post_filter_device(out.data_ptr(), stream=st)
+        if self.lk_refine:
+            self.sgm.lk_refine_device(d_left, d_right, out.data_ptr(), stream=st)
+        return out

@@ -37,7 +37,7 @@ class SGM:
                  blur: bool = True, views: int = 2, p1: int = 10, p2: int = 100,
                  uniqueness: float = 0.7, lr_max_diff: float = 1.0, post_filter: bool = False,
                  lk_refine: bool = False, sky_detect: bool = False,
-                 aux_only: bool = False, _solver: int = _capi.SGM_SOLVER_SGM):
+                 aux_only: bool = False, view: str = "left", _solver: int = _capi.SGM_SOLVER_SGM):
         self._lib = lib()
         p = _capi.default_params(h, w, s, d)
         p.blur = int(bool(blur))
@@ -52,6 +52,11 @@ class SGM:
         p.solver = _solver
         # aux_only: side stages only (sky, post_filter, LKRefine, colormap, cloud)
         p.aux_only = int(bool(aux_only))
+        # view ("left" | "right", views=1 only): the right view alone (SGM.cpp:448-801),
+        # for a pair split over two GPUs that meet in lr_check_device
+        if view not in ("left", "right"):
+            raise ValueError(f"view must be 'left' or 'right', got {view!r}")
+        p.view = _capi.SGM_VIEW_RIGHT if view == "right" else _capi.SGM_VIEW_LEFT
         p.p1, p.p2 = p1, p2
         p.uniqueness, p.lr_max_diff = uniqueness, lr_max_diff
         self.params = p
@@ -126,6 +131,17 @@ class SGM:
         if self._lr is None:
             raise RuntimeError("constructed with post_filter=True: only get_disp() is kept")
         return self._lr
+
+    def lr_check_device(self, d_fl: int, d_fr: int, d_out: int, *, fl_pitch: int | None = None,
+                        fr_pitch: int | None = None, out_pitch: int | None = None,
+                        stream: int = 0) -> None:
+        """The LR check (SGM.cpp:803-818) of two device sub-pixel maps, e.g.
+        the left and right views computed on two GPUs (sgm_lr_check_device);
+        d_out may be d_fl."""
+        check(self._lib.sgm_lr_check_device(
+            self._h, ctypes.c_void_p(d_fl), fl_pitch or self.cols, ctypes.c_void_p(d_fr),
+            fr_pitch or self.cols, ctypes.c_void_p(d_out), out_pitch or self.cols,
+            ctypes.c_void_p(stream or None)), self._h)
 
     def post_filter(self, disp) -> np.ndarray:
         """post_filter() (Solver.cpp:600-649) of a rows x cols map on the GPU
@@ -202,7 +218,8 @@ class SGM:
         return xyz[:n.value].copy(), pix[:n.value].copy()
 
     def get_raw_disp(self) -> np.ndarray:
-        """Left WTA disparity (SGM.cpp:411-415), uint16, invalid = D+1."""
+        """Left WTA disparity (SGM.cpp:411-415; disp_beta, :755-795, for a
+        right-view handle), uint16, invalid = D+1."""
         return self._raw
 
     # ---------------------------------------------------------- profiling

@@ -53,6 +53,7 @@ def test_default_params_are_the_reference_constants(lib):
     assert abs(p.uniqueness - 0.7) < 1e-7           # inc/Solver.h:14
     assert p.lr_max_diff == 1.0                     # inc/Solver.h:16
     assert p.blur == 1 and p.views == 2 and p.scale == 1 and p.max_disp == 128
+    assert p.view == _capi.SGM_VIEW_LEFT and p.post_filter == 0 and p.aux_only == 0
 
 
 @pytest.mark.parametrize("h,w,s,d", [(375, 1242, 3, 128), (375, 1242, 1, 96), (0, 10, 1, 32),
@@ -67,14 +68,19 @@ def test_invalid_arguments_rejected(lib, h, w, s, d):
     assert not handle.value
 
 
-@pytest.mark.parametrize("field,value,h,w", [("solver", 7, 375, 1242), ("sky_detect", 1, 100, 9000),
-                                             ("sky_detect", 1, 5000, 100), ("views", 3, 375, 1242)])
-def test_invalid_stage_parameters_rejected(lib, field, value, h, w):
-    # parameters of the section-8f stages are checked at sgm_create, before
-    # any device work (sky detector limits: sgm_sky.hip)
+@pytest.mark.parametrize("fields", [{"solver": 7}, {"sky_detect": 1, "width": 9000, "height": 100},
+                                    {"sky_detect": 1, "height": 5000, "width": 100}, {"views": 3},
+                                    {"view": 2}, {"view": 1},                      # views == 2
+                                    {"view": 1, "views": 1, "post_filter": 1},
+                                    {"view": 1, "views": 1, "lk_refine": 1},
+                                    {"view": 1, "views": 1, "solver": 1}])
+def test_invalid_stage_parameters_rejected(lib, fields):
+    # parameters of the section-8f stages and of the view split are checked
+    # at sgm_create, before any device work (sky detector limits: sgm_sky.hip)
     p = _capi.Params()
-    lib.sgm_default_params(ctypes.byref(p), h, w, 1, 64)
-    setattr(p, field, value)
+    lib.sgm_default_params(ctypes.byref(p), 375, 1242, 1, 64)
+    for field, value in fields.items():
+        setattr(p, field, value)
     handle = ctypes.c_void_p()
     assert lib.sgm_create(ctypes.byref(p), 0, ctypes.byref(handle)) == _capi.SGM_ERR_INVALID_ARG
     assert not handle.value
@@ -85,7 +91,8 @@ def test_stage_entry_points_reject_null(lib):
                       ("sgm_sky_detect_device", 6), ("sgm_colormap_device", 6),
                       ("sgm_point_cloud_device", 10), ("sgm_stage_post_filter", 2),
                       ("sgm_stage_lk_refine", 5), ("sgm_stage_sky_detect", 4),
-                      ("sgm_stage_colormap", 3), ("sgm_stage_point_cloud", 8)):
+                      ("sgm_stage_colormap", 3), ("sgm_stage_point_cloud", 8),
+                      ("sgm_lr_check_device", 8)):
         f = getattr(lib, fn)
         assert len(f.argtypes) == nargs, fn
         args = [0 if t is ctypes.c_int else None for t in f.argtypes]

@@ -109,3 +109,67 @@ def test_pipelined_gather_world2_gloo():
     for k, maps in res[0].items():
         for r in range(2):
             assert (maps[r] == 100 * r + k).all(), (k, r)
+
+
+class _OracleView:
+    """Stands in for an SGM view handle on CPU: the oracle's left or right
+    sub-pixel map written through the data pointers ViewSplit passes."""
+
+    def __init__(self, view):
+        self.view = view
+
+    @staticmethod
+    def _at(ptr, ctype, shape):
+        import ctypes
+        n = int(np.prod(shape))
+        return np.ctypeslib.as_array((ctype * n).from_address(ptr)).reshape(shape)
+
+    def process_device(self, d_left, d_right, d_out, stream=0):
+        import ctypes
+        import oracle
+        left = self._at(d_left, ctypes.c_uint8, (H, W)).copy()
+        right = self._at(d_right, ctypes.c_uint8, (H, W)).copy()
+        ref = oracle.process(left, right, D)
+        self._at(d_out, ctypes.c_float, (H, W))[:] = ref["sub_beta" if self.view else "sub"]
+
+    def lr_check_device(self, d_fl, d_fr, d_out, stream=0):
+        import ctypes
+        import pyref
+        fl = self._at(d_fl, ctypes.c_float, (H, W)).copy()
+        fr = self._at(d_fr, ctypes.c_float, (H, W)).copy()
+        self._at(d_out, ctypes.c_float, (H, W))[:] = pyref.lr_check(fl, fr, D)
+
+
+def _split_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        team = distributed.ViewSplit(_OracleView(rank % 2), H, W, "cpu")
+        left, right = (torch.from_numpy(a) for a in synthetic.stereo_pair(H, W, D, rank // 2))
+        out = team.step(left.data_ptr(), right.data_ptr())
+        q.put((rank, None if out is None else out.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_view_split_world4_gloo():
+    # two teams of (left view, right view): each even rank ends with the LR-
+    # checked map of its team's pair, built from the partner's F_R
+    import oracle
+    oracle.build()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None and res[3] is None
+    for team in range(2):
+        ref = oracle.process(*synthetic.stereo_pair(H, W, D, team), D)
+        assert np.array_equal(res[2 * team].view(np.uint32), ref["lr"].view(np.uint32)), team
