@@ -100,6 +100,18 @@ def algorithmic_bytes(name: str, elems: float, D: int) -> float:
     return bytes_per_elem(name, D) * elems
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (SURVEY.md 8d asks for it beside the baseline)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -302,7 +314,7 @@ def main():
         stages = ("sky detector + SGM + LR + post_filter + LKRefine" if full else
                   "SGM" + (" + LR + post_filter" if views == 2 else ""))
         cpu = {"value": round(views * sh * w * D / tmed / 1e6, 2), "unit": "Mpixel-disparities/s",
-               "cores": oracle.max_threads(), "kind": "port",
+               "cores": oracle.max_threads(), "kind": "port", "cpu_model": cpu_model(),
                "sample": f"{len(ts)} {what} of the same workload ({w}x{h} D={D}, V={views}; "
                          f"{stages}) through oracle/sgm_oracle.c (C restatement, OpenMP "
                          f"placement of the reference), median {tmed:.3f} s per sample"}
@@ -312,6 +324,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "Mpixel-disparities/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+            "pairs_per_s": round(pairs * args.steps / elapsed, 2),
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": cfg["workload"] if cfg.get("full") else
                        cfg["workload"] + (" + sky detector" if args.sky_detect else "")
