@@ -60,8 +60,9 @@ def main():
         data = json.load(open(path))
     data[cfg] = {k: v["bytes"] for k, v in out.items()}
     data.setdefault("_detail", {})[cfg] = out
-    data["_source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, tag {tag}; "
-                       "FETCH_SIZE doubled (gfx950), KiB -> bytes; per-launch means")
+    data.setdefault("_tags", {})[cfg] = tag
+    data["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (run tag per "
+                       "config in _tags); FETCH_SIZE doubled (gfx950), KiB -> bytes; per-launch means")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
     for k, v in out.items():
