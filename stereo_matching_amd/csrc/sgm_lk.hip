@@ -8,10 +8,12 @@
 // Ix = (L(j+1) - L(j-1)) * 0.5 and the left pixels -- are staged in LDS for
 // the tile plus a 3-pixel apron; the right-image samples R(m, n - d) move
 // with the offset and are gathered from global memory, all 49 in flight at
-// once, into registers.  An iteration makes three passes over the window:
-// (A) validity, sum w^2 and the right samples, (B) the Hessian, (C) the offset.  Zero-weight slots are skipped: adding +0 (or
-// -0) never changes an fp32 sum, so the sums equal the reference's 49-term
-// ones.
+// once, into registers.  The slot tests that do not depend on the offset
+// are made once per pixel; an iteration then makes up to three passes over
+// the window: (A) the image-edge test, sum w^2 and the right samples, (B) the
+// Hessian, only when the set of valid slots changed (it is a function of that
+// set), (C) the offset.  Zero-weight slots are skipped: adding +0 (or -0)
+// never changes an fp32 sum, so the sums equal the reference's 49-term ones.
 #include "sgm_device.h"
 
 namespace sgm {
@@ -65,6 +67,21 @@ __global__ __launch_bounds__(kLkThreads) void lk_refine_kernel(
         const float wc = 0.36787945f;            // (float)exp(-1): corner slots (:154)
         const float wc2 = wc * wc;
         float last_disp = d0, last_doff = 0.f, last_diff = FLT_MAX;
+        // the slot tests that do not move with the offset (:131-140):
+        // gradient, disparity range, |d0 - dm| <= 2
+        unsigned long long fixed = 0;
+#pragma unroll
+        for (int k = 0; k < 49; ++k) {
+            const int v = k / 7 - kLkHW, u = k % 7 - kLkHW;
+            const float ix = ixT[ar + v][ac + u];
+            const float dm = dtT[ar + v][ac + u];
+            if (ix > 2.f && dm > 0.f && dm < fD && !(fabsf(d0 - dm) > 2.f)) fixed |= 1ull << k;
+        }
+        // the Hessian depends only on the set of valid slots; only the
+        // image-edge test moves with the offset, so after the first iteration
+        // it is usually reused (bit-identical: the same sum over the same set)
+        unsigned long long hs_valid = ~0ull;     // no set of 49 slots is all ones
+        float hs = 0.f;
         for (int it = 0; it < 10; ++it) {        // iter_num (LKSubPixelImpl.h:46)
             // (A) the window (:114-163): valid slots and sum w^2, then the
             // right samples, all 49 loads issued before any is used
@@ -75,12 +92,10 @@ __global__ __launch_bounds__(kLkThreads) void lk_refine_kernel(
 #pragma unroll
             for (int k = 0; k < 49; ++k) {
                 const int v = k / 7 - kLkHW, u = k % 7 - kLkHW;
-                const float ix = ixT[ar + v][ac + u];
                 const float dm = dtT[ar + v][ac + u];
                 const int n = j + u;
                 const float x = (float)n - (dm + last_doff);
-                const bool ok = ix > 2.f && dm > 0.f && dm < fD && !(fabsf(d0 - dm) > 2.f) &&
-                                !(x < 0.f || x > (float)(W - 1));
+                const bool ok = ((fixed >> k) & 1) && !(x < 0.f || x > (float)(W - 1));
                 rx[k] = ok ? (int)x : j;  // a safe column for the skipped slots
                 if (ok) {
                     valid |= 1ull << k;
@@ -98,13 +113,16 @@ __global__ __launch_bounds__(kLkThreads) void lk_refine_kernel(
             const float nrm = sqrtf(s2);         // win_weight.norm() (:172)
             const float wn1 = 1.f / nrm, wnc = wc / nrm;
             // (B) Hessian = (J^T W) J (:176)
-            float hs = 0.f;
+            if (valid != hs_valid) {
+                hs_valid = valid;
+                hs = 0.f;
 #pragma unroll
-            for (int k = 0; k < 49; ++k) {
-                if (!((valid >> k) & 1)) continue;
-                const int v = k / 7 - kLkHW, u = k % 7 - kLkHW;
-                const float ix = ixT[ar + v][ac + u];
-                hs += (ix * ((v * v + u * u >= 18) ? wnc : wn1)) * ix;
+                for (int k = 0; k < 49; ++k) {
+                    if (!((valid >> k) & 1)) continue;
+                    const int v = k / 7 - kLkHW, u = k % 7 - kLkHW;
+                    const float ix = ixT[ar + v][ac + u];
+                    hs += (ix * ((v * v + u * u >= 18) ? wnc : wn1)) * ix;
+                }
             }
             if ((double)hs < 1e-3) break;        // :178 (Hessian(0,0) < 1e-3, a double)
             // (C) doff = ((H^-1 J^T) W) Ires (:185)
