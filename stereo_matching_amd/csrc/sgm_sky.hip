@@ -10,11 +10,12 @@
 // runs narrower than 30.  Five launches, no host round trip:
 //   1. gray:    working-grid image (2x2 average at scale 2) + moments of all
 //               non-zero pixels;
-//   2. columns: one thread per column scans the top half once: a row whose
-//               |grad|^2 exceeds the next thresholds' t^2 is their border
-//               (or -1), recorded with the sky moments above it; the first
-//               dark (< 128) row; then one workgroup per threshold sums the
-//               columns' sky moments;
+//   2. columns: per (row, column) the number of thresholds whose t^2 its
+//               |grad|^2 exceeds; then one thread per column walks the top
+//               half once: a row whose count exceeds every earlier row's is
+//               the border (or -1) of the new thresholds, recorded with the
+//               sky moments above it; the first dark (< 128) row; then one
+//               workgroup per threshold sums the columns' sky moments;
 //   3. select:  one workgroup: energies, the first maximum, the gray-value
 //               and isolated-column checks (parallel: a dropped isolated
 //               column can never enable its right neighbour's drop), and the
@@ -28,10 +29,6 @@ namespace {
 constexpr int kSkyT = 120;            // thresholds: floor((600-5)/5)+1 (:248-249)
 constexpr int kSkyMaxW = 8192;        // widest working grid the select kernel holds in LDS
 constexpr size_t kSkyTotBytes = 4096; // scratch header: 3 x (kSkyT + 1) u64 totals
-__device__ __forceinline__ long long sky_t2(int k) {  // t_k^2, t_k = 5 + 3k (:259-263)
-    const long long t = 5 + 3 * k;
-    return t * t;
-}
 
 // One detection's buffers; launches take both views and pick theirs by the
 // workgroup's z index (node.cpp:83-86 detects on both images).
@@ -95,23 +92,73 @@ __device__ __forceinline__ int reflect101(int x, int n) {  // BORDER_REFLECT_101
 
 // 2. per column: the border of every threshold (extract_border, :288-343) with
 // the sky moments above it (calculate_sky_energy, :633-646), the first dark
-// row (check_sky_border_by_gray_value, :101-109).  A workgroup owns 64
-// columns: its four waves first stage the top-half strip (rows 0..half+1,
-// columns c0-1..c0+64 at reflected coordinates, plus columns W-1 and 0 for the
-// row-wrapping grad_y probe of the edge columns) in LDS, then wave 0 scans it,
-// one lane per column.
-constexpr int kSkyStripW = 68;  // 66 window columns, then G[r][W-1], G[r][0]
+// row (check_sky_border_by_gray_value, :101-109).  A workgroup owns 16
+// columns.  Its four waves stage the top-half strip (rows 0..half+1, columns
+// c0-1..c0+16 at reflected coordinates, plus columns W-1 and 0 for the
+// row-wrapping grad_y probe of the edge columns) in LDS.  Then, per column
+// and group of 16 rows, they compute every row's count of the thresholds its
+// |grad|^2 exceeds, and the group's largest count and sky moments.  The
+// border of threshold k is the first row whose count exceeds k, so one lane
+// per column walks its groups: a group whose largest count resolves no new
+// threshold only adds its moments; in the others, a row whose count exceeds
+// every earlier row's is the border of the new thresholds, whose results
+// (border or -1, the moments of the rows above it) go to an LDS table.  All
+// threads then write the table out, one coalesced row of columns per
+// threshold.
+constexpr int kSkyCols = 16;             // columns per workgroup
+constexpr int kSkyStripW = kSkyCols + 4; // 18 window columns, then G[r][W-1], G[r][0]
+constexpr int kSkyGrp = 16;              // rows per group
 constexpr size_t kSkyStripMax = 160 * 1024 - 1024;
+// #{k < kSkyT : t_k^2 < a}, thresholds t_k = 5 + 3k (:259-263)
+__device__ __forceinline__ int sky_count(int a) {
+    if (a <= 25) return 0;                          // t_0 = 5
+    const int x = a - 1;                            // t^2 < a  <=>  t <= isqrt(a - 1)
+    int q = (int)sqrtf((float)x);
+    while (q * q > x) --q;
+    while ((q + 1) * (q + 1) <= x) ++q;
+    const int n = (q - 5) / 3 + 1;                  // t_k = 5 + 3k <= q
+    return n < kSkyT ? n : kSkyT;
+}
+#ifdef SGM_STAMPS
+__device__ unsigned long long sky_stamps[4];  // staging, counts, walk + table cycles; blocks
+#endif
+// LDS layout: strip [last+2][kSkyStripW] u8 | (16 B aligned) counts
+// [kSkyCols][ngrp] x 16 u8 | group stats [kSkyCols][ngrp] int4 (largest count,
+// n, s1, s2) | results [kSkyT][kSkyCols] int4 | first dark row, resolved
+// thresholds per column
+struct SkyLds {
+    size_t counts, stats, table, dark, done, bytes;
+    __host__ __device__ SkyLds(int last) {
+        const size_t ngrp = (size_t)(last + kSkyGrp) / kSkyGrp;
+        counts = ((size_t)(last + 2) * kSkyStripW + 15) & ~(size_t)15;
+        stats = counts + 16 * kSkyCols * ngrp;
+        table = stats + 16 * kSkyCols * ngrp;
+        dark = table + (size_t)16 * kSkyT * kSkyCols;
+        done = dark + 4 * kSkyCols;
+        bytes = done + 4 * kSkyCols;
+    }
+};
 __global__ __launch_bounds__(256) void sky_columns_kernel(SkyViews sv, int H, int W) {
     const SkyView &V = sv.v[bid_z()];
     const uint8_t *__restrict__ G = V.G;
     int *__restrict__ B = V.B;
     int *__restrict__ M = V.M;
     int *__restrict__ dark = V.dark;
-    extern __shared__ uint8_t strip[];  // [rows 0..last+1][kSkyStripW]
-    const int c0 = bid_x() * 64, t = tid_x();
+    extern __shared__ uint8_t strip[];
+    const int c0 = bid_x() * kSkyCols, t = tid_x();
+#ifdef SGM_STAMPS
+    const long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
     const int half = H / 2, last = half < H - 1 ? half : H - 1;
     const int nrows = last + 2 < H ? last + 2 : H;  // rows 0..last+1 that exist
+    const int ngrp = (last + kSkyGrp) / kSkyGrp;
+    const SkyLds lay(last);
+    uint4 *counts = reinterpret_cast<uint4 *>(strip + lay.counts);
+    int4 *stats = reinterpret_cast<int4 *>(strip + lay.stats);
+    int4 *table = reinterpret_cast<int4 *>(strip + lay.table);
+    int *darkL = reinterpret_cast<int *>(strip + lay.dark);
+    int *kdone = reinterpret_cast<int *>(strip + lay.done);
+    if (t < kSkyCols) darkL[t] = H;
     // 8 loads in flight per thread before their LDS stores
     const int total = nrows * kSkyStripW;
     for (int q0 = 0; q0 < total; q0 += 8 * 256) {
@@ -120,7 +167,7 @@ __global__ __launch_bounds__(256) void sky_columns_kernel(SkyViews sv, int H, in
         for (int u = 0; u < 8; ++u) {
             const int q = q0 + u * 256 + t;
             const int r = q / kSkyStripW, x = q - r * kSkyStripW;
-            const int col = x < 66 ? reflect101(c0 - 1 + x, W) : (x == 66 ? W - 1 : 0);
+            const int col = x < kSkyCols + 2 ? reflect101(c0 - 1 + x, W) : (x == kSkyCols + 2 ? W - 1 : 0);
             v[u] = q < total ? G[(size_t)r * W + col] : 0;
         }
 #pragma unroll
@@ -130,68 +177,117 @@ __global__ __launch_bounds__(256) void sky_columns_kernel(SkyViews sv, int H, in
         }
     }
     __syncthreads();
-    if (t >= 64) return;
-    const int c = c0 + t;
-    if (c >= W) return;
-    const size_t kW = (size_t)kSkyT * W;
-    auto row3 = [&](int r) {  // (G[r][c-1], G[r][c], G[r][c+1]) packed, reflected
-        const uint8_t *q = strip + reflect101(r, H) * kSkyStripW + t;
-        return (int)q[0] | ((int)q[1] << 8) | ((int)q[2] << 16);
-    };
-    // |Sobel|^2 of row r from rows r-1, r, r+1 (ksize 3, :215-232)
-    auto sob2 = [](int pv, int cu, int nv) {
-        const int dx = (((pv >> 16) & 255) + 2 * ((cu >> 16) & 255) + ((nv >> 16) & 255)) -
-                       ((pv & 255) + 2 * (cu & 255) + (nv & 255));
-        const int dy = ((nv & 255) + 2 * ((nv >> 8) & 255) + ((nv >> 16) & 255)) -
-                       ((pv & 255) + 2 * ((pv >> 8) & 255) + ((pv >> 16) & 255));
-        return (long long)(dx * dx + dy * dy);
-    };
-    // Thresholds in increasing order: the first row whose |grad|^2 > t_k^2
-    // never moves up as k grows, so one pointer walks the column once; the
-    // moments of the rows above it are the sky moments of that border.
-    int r = 0, n = 0, s1 = 0, s2 = 0, fd = H;
-    int pv = row3(-1), cu = row3(0), nv = row3(1);
-    long long a = sob2(pv, cu, nv);
-    for (int k = 0; k < kSkyT; ++k) {
-        const long long t2 = sky_t2(k);
-        while (r <= last && !(a > t2)) {
-            const int g = (cu >> 8) & 255;
-            if (g < 128 && fd == H) fd = r;
-            if (g) { ++n; s1 += g; s2 += g * g; }
-            ++r;
-            pv = cu;
-            cu = nv;
-            nv = row3(r + 1);
-            a = sob2(pv, cu, nv);
-        }
-        int b = -1;
-        if (r <= last && r < half && r > 5) {
-            // grad_y (:309-314) reads (r +- 1, c +- 1) by row-major flat index
-            // (cv::Mat::at): the register window for inner columns; at the edge
-            // columns the index wraps into the neighbouring row
-            const uint8_t *sr = strip + t + 1;  // (row 0, column c)
-            auto S = [&](int rr, int dc) { return (int)sr[rr * kSkyStripW + dc]; };
-            int gy;
-            if (c > 0 && c < W - 1) {
-                gy = (2 * ((nv >> 8) & 255) + ((nv >> 16) & 255) + (nv & 255)) -
-                     (2 * ((pv >> 8) & 255) + ((pv >> 16) & 255) + (pv & 255));
-            } else if (c == 0) {  // (r+1, -1) = (r, W-1); (r-1, -1) = (r-2, W-1)
-                gy = (2 * S(r + 1, 0) + S(r + 1, 1) + (int)strip[r * kSkyStripW + 66]) -
-                     (2 * S(r - 1, 0) + S(r - 1, 1) + (int)strip[(r - 2) * kSkyStripW + 66]);
-            } else {              // (r+1, W) = (r+2, 0); (r-1, W) = (r, 0)
-                gy = (2 * S(r + 1, 0) + (int)strip[(r + 2) * kSkyStripW + 67] + S(r + 1, -1)) -
-                     (2 * S(r - 1, 0) + (int)strip[r * kSkyStripW + 67] + S(r - 1, -1));
+#ifdef SGM_STAMPS
+    const long long ts1 = __builtin_amdgcn_s_memtime();
+#endif
+    // per (column, group of 16 rows): |Sobel|^2 (ksize 3, :215-232) of each
+    // row from rows r-1, r, r+1 at reflected coordinates, as the count of
+    // thresholds it exceeds; the group's largest count and moments; the
+    // column's first dark row
+    for (int q = t; q < ngrp * kSkyCols; q += 256) {
+        const int x = q % kSkyCols, grp = q / kSkyCols;
+        unsigned w[4] = {0, 0, 0, 0};
+        int mx = 0, n = 0, s1 = 0, s2 = 0, fd = H;
+#pragma unroll
+        for (int i = 0; i < kSkyGrp; ++i) {
+            const int r = grp * kSkyGrp + i;
+            if (r <= last) {
+                const uint8_t *p = strip + reflect101(r - 1, H) * kSkyStripW + x;
+                const uint8_t *m = strip + r * kSkyStripW + x;
+                const uint8_t *nx = strip + reflect101(r + 1, H) * kSkyStripW + x;
+                const int dx = ((int)p[2] + 2 * m[2] + nx[2]) - ((int)p[0] + 2 * m[0] + nx[0]);
+                const int dy = ((int)nx[0] + 2 * nx[1] + nx[2]) - ((int)p[0] + 2 * p[1] + p[2]);
+                const int k = sky_count(dx * dx + dy * dy);
+                w[i >> 2] |= (unsigned)k << (8 * (i & 3));
+                mx = k > mx ? k : mx;
+                const int g = m[1];
+                if (g) { ++n; s1 += g; s2 += g * g; }
+                if (g < 128 && fd == H) fd = r;
             }
-            b = gy > 0 ? -1 : r;
         }
-        B[(size_t)k * W + c] = b;
-        M[(size_t)k * W + c] = b < 0 ? 0 : n;
-        M[kW + (size_t)k * W + c] = b < 0 ? 0 : s1;
-        M[2 * kW + (size_t)k * W + c] = b < 0 ? 0 : s2;
+        counts[x * ngrp + grp] = make_uint4(w[0], w[1], w[2], w[3]);
+        stats[x * ngrp + grp] = make_int4(mx, n, s1, s2);
+        if (fd < H) atomicMin(&darkL[x], fd);
     }
-    for (; r <= last && fd == H; ++r)  // the first dark row of the top half
-        if ((int)strip[r * kSkyStripW + t + 1] < 128) fd = r;
-    dark[c] = fd;
+    __syncthreads();
+#ifdef SGM_STAMPS
+    const long long ts2 = __builtin_amdgcn_s_memtime();
+#endif
+    const int c = c0 + t;
+    if (t < kSkyCols && c < W) {
+        const uint8_t *sr = strip + t + 1;  // (row 0, column c)
+        auto S = [&](int rr, int dc) { return (int)sr[rr * kSkyStripW + dc]; };
+        int kcur = 0, n = 0, s1 = 0, s2 = 0;
+        for (int grp = 0; grp < ngrp; ++grp) {
+            const int4 st = stats[t * ngrp + grp];
+            if (st.x <= kcur) {  // no row of the group resolves a new threshold
+                n += st.y;
+                s1 += st.z;
+                s2 += st.w;
+                continue;
+            }
+            const uint4 kq = counts[t * ngrp + grp];
+            const unsigned kw[4] = {kq.x, kq.y, kq.z, kq.w};
+            int gv[kSkyGrp];
+#pragma unroll
+            for (int i = 0; i < kSkyGrp; ++i) {
+                const int r = grp * kSkyGrp + i;
+                gv[i] = r <= last ? S(r, 0) : 0;
+            }
+#pragma unroll
+            for (int i = 0; i < kSkyGrp; ++i) {
+                const int r = grp * kSkyGrp + i;
+                const int kr = (kw[i >> 2] >> (8 * (i & 3))) & 255;  // 0 past the last row
+                if (kr > kcur) {  // the border of thresholds kcur..kr-1
+                    int b = -1;
+                    if (r < half && r > 5) {
+                        // grad_y (:309-314) reads (r +- 1, c +- 1) by row-major flat
+                        // index (cv::Mat::at): at the edge columns the index wraps
+                        // into the neighbouring row
+                        int gy;
+                        if (c > 0 && c < W - 1) {
+                            gy = (2 * S(r + 1, 0) + S(r + 1, 1) + S(r + 1, -1)) -
+                                 (2 * S(r - 1, 0) + S(r - 1, 1) + S(r - 1, -1));
+                        } else if (c == 0) {  // (r+1, -1) = (r, W-1); (r-1, -1) = (r-2, W-1)
+                            gy = (2 * S(r + 1, 0) + S(r + 1, 1) + S(r, kSkyCols + 1 - t)) -
+                                 (2 * S(r - 1, 0) + S(r - 1, 1) + S(r - 2, kSkyCols + 1 - t));
+                        } else {              // (r+1, W) = (r+2, 0); (r-1, W) = (r, 0)
+                            gy = (2 * S(r + 1, 0) + S(r + 2, kSkyCols + 2 - t) + S(r + 1, -1)) -
+                                 (2 * S(r - 1, 0) + S(r, kSkyCols + 2 - t) + S(r - 1, -1));
+                        }
+                        b = gy > 0 ? -1 : r;
+                    }
+                    const int4 e = b < 0 ? make_int4(-1, 0, 0, 0) : make_int4(b, n, s1, s2);
+                    for (; kcur < kr; ++kcur) table[kcur * kSkyCols + t] = e;
+                }
+                const int g = gv[i];
+                if (g) { ++n; s1 += g; s2 += g * g; }
+            }
+        }
+        kdone[t] = kcur;  // thresholds kcur.. have no border in the top half
+        dark[c] = darkL[t];
+    }
+    __syncthreads();
+    const size_t kW = (size_t)kSkyT * W;
+    for (int q = t; q < kSkyT * kSkyCols; q += 256) {
+        const int k = q / kSkyCols, x = q - k * kSkyCols, cc = c0 + x;
+        if (cc >= W) continue;
+        const int4 e = k < kdone[x] ? table[q] : make_int4(-1, 0, 0, 0);
+        const size_t o = (size_t)k * W + cc;
+        B[o] = e.x;
+        M[o] = e.y;
+        M[kW + o] = e.z;
+        M[2 * kW + o] = e.w;
+    }
+#ifdef SGM_STAMPS
+    const long long ts3 = __builtin_amdgcn_s_memtime();
+    if (t == 0) {
+        atomicAdd(&sky_stamps[0], (unsigned long long)(ts1 - ts0));
+        atomicAdd(&sky_stamps[1], (unsigned long long)(ts2 - ts1));
+        atomicAdd(&sky_stamps[2], (unsigned long long)(ts3 - ts2));
+        atomicAdd(&sky_stamps[3], 1ull);
+    }
+#endif
 }
 
 // 2b. per threshold k < kSkyT: the sums of the columns' sky moments; block
@@ -355,12 +451,13 @@ hipError_t launch_sky_detect(const uint8_t *const *img, int pitch, uint8_t *cons
     const dim3 gridg((g.W + 63) / 64, (g.H + 15) / 16, nviews);
     hipLaunchKernelGGL(sky_gray_kernel, gridg, dim3(256), 0, st, sv, pitch, g.scale, g.H, g.W);
     const int half = g.H / 2, last = half < g.H - 1 ? half : g.H - 1;
-    const size_t strip = (size_t)(last + 2) * kSkyStripW;
+    const size_t strip = SkyLds(last).bytes;
     if (strip > kSkyStripMax) return hipErrorInvalidValue;  // H > ~4700 rows
     hipError_t e = hipFuncSetAttribute((const void *)sky_columns_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)strip);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + 63) / 64, 1, nviews), dim3(256), strip, st,
+    hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + kSkyCols - 1) / kSkyCols, 1, nviews),
+                       dim3(256), strip, st,
                        sv, g.H, g.W);
     hipLaunchKernelGGL(sky_reduce_kernel, dim3(kSkyT + 1, 1, nviews), dim3(256), 0, st, sv, g.W,
                        (int)(gridg.x * gridg.y));
@@ -371,3 +468,15 @@ hipError_t launch_sky_detect(const uint8_t *const *img, int pitch, uint8_t *cons
 }
 
 }  // namespace sgm
+
+#ifdef SGM_STAMPS
+extern "C" int sgm_debug_stamps_sky(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sgm::sky_stamps), sizeof(sgm::sky_stamps)) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[4] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(sgm::sky_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
