@@ -438,6 +438,18 @@ __device__ __forceinline__ Wta wta_dpp(const Wta &x) {
     return wta_merge(x, y);
 }
 
+// Merge with the lane 16 apart inside each 32-lane half (ds_swizzle bit mode,
+// xor_mask 0x10): the cross-row step when a pixel spans 32 lanes.
+__device__ __forceinline__ Wta wta_swz16(const Wta &x) {
+    constexpr int PAT = 0x1F | (0x10 << 10);
+    Wta y;
+    y.m = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x.m), PAT));
+    y.s = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x.s), PAT));
+    y.i = __builtin_amdgcn_ds_swizzle(x.i, PAT);
+    y.si = __builtin_amdgcn_ds_swizzle(x.si, PAT);
+    return wta_merge(x, y);
+}
+
 // LDS image of one chunk: PF pixels x D total costs, rows padded by 16 bytes
 // so the consumer's per-pixel reads spread over all banks.
 template <int V>
@@ -478,6 +490,8 @@ __device__ __forceinline__ void wta_consume_chunk_at(const float (*tb)[tbuf_stri
     w = wta_dpp<DPP_QP_2301>(w);
     if (LPP >= 8) w = wta_dpp<DPP_HALF_MIRROR>(w);
     if (LPP >= 16) w = wta_dpp<DPP_MIRROR>(w);
+    if (LPP >= 32) w = wta_swz16(w);
+    static_assert(LPP <= 32, "a pixel spans at most 32 lanes");
     int d = w.i;
     if (w.s != SGM_INF && w.m / w.s > uniq && abs(w.i - w.si) > 1) d = Dn + 1;
     float f;

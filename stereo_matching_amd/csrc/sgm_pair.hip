@@ -145,9 +145,9 @@ __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
 // S12 and T, then WTA.  Three waves (pair_split_body): wave 0 recomputes L3
 // segments from their checkpoints, wave 1 runs L4 and sums the totals into an
 // LDS ring, wave 2 runs the batched WTA on the chunk before.
-// D = 64 / 128 run two WTA waves per column (four pixels each per chunk).
+// D >= 64 run two WTA waves per column (each takes half of a chunk's pixels).
 template <int V, bool FULL>
-constexpr int final_nwta() { return FULL && V <= 2 ? 2 : 1; }
+constexpr int final_nwta() { return FULL ? 2 : 1; }
 
 template <int V, bool FULL>
 __global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {

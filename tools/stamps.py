@@ -1,6 +1,6 @@
 """Barrier-wait breakdown of the split pair kernels (library built with
 -DSGM_STAMPS).  Runs a few K128 frames and prints, per wave role, the mean
-work and barrier-wait cycles per wave."""
+work and barrier-wait cycles per wave.  Usage: stamps.py [H W D]."""
 import ctypes
 import os
 import sys
@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from stereo_matching_amd import SGM, synthetic, _capi  # noqa: E402
 
-h, w, D = 375, 1242, 128
+h, w, D = (int(x) for x in sys.argv[1:4]) if len(sys.argv) > 3 else (375, 1242, 128)
 left, right = synthetic.stereo_pair(h, w, D, pair_index=0)
 dev = torch.device("cuda", 0)
 dl, dr = torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev)
