@@ -47,11 +47,17 @@ __device__ __forceinline__ int blur_at(const uint8_t *src, int rpitch, int step,
     return v > 255 ? 255 : v;
 }
 
-constexpr int CT_TW = 64, CT_TH = 8;
+constexpr int CT_TW = 64, CT_TH = 16, CT_RPT = CT_TH / 4;  // 4 waves x CT_RPT rows
 
-// CT_pts (cost.cpp:99-129) for one image; window (7/s) x (9/s), MSB first,
-// centre skipped, coordinates clamped to the (working-grid) edge.  The
-// (blurred) window is staged in LDS at clamped coordinates.
+// CT_pts (cost.cpp:99-129) for one image; window (2HH+1) x (2HWW+1) = 7x9 (3x5
+// at scale 2), MSB first, centre skipped, coordinates clamped to the
+// (working-grid) edge.  A workgroup owns a 64 x 16 pixel tile:
+//   1. the raw pixels the blur of the tile + census apron needs are loaded
+//      once (rows/columns lo-1 .. hi+1 at BORDER_REFLECT_101 coordinates);
+//   2. the blurred window is built in LDS at clamped coordinates from them;
+//   3. each lane walks CT_RPT consecutive rows of its column: every window
+//      row is read once and feeds the census words of all the rows whose
+//      window holds it (bits appended in row-major order, as the reference).
 // Both images in one launch: workgroup z selects (src0, ct0) or (src1, ct1).
 template <int HH, int HWW>
 __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__ src0,
@@ -63,29 +69,89 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
     const uint8_t *__restrict__ src = second ? src1 : src0;
     uint64_t *__restrict__ ct = second ? ct1 : ct0;
     constexpr int TR = CT_TH + 2 * HH, TC = CT_TW + 2 * HWW;
+    constexpr int RR = TR + 2, RC = TC + 2;       // raw staging bound
+    constexpr int RAW_IT = (RR * RC + 255) / 256;
     __shared__ uint8_t tile[TR][TC];
+    __shared__ uint8_t raw[RR][RC];
     const int x0 = bid_x() * CT_TW, y0 = bid_y() * CT_TH;
-    for (int idx = tid_x(); idx < TR * TC; idx += 256) {
-        const int ty = idx / TC, tx = idx - ty * TC;
-        const int y = clampi(y0 + ty - HH, 0, H - 1), x = clampi(x0 + tx - HWW, 0, W - 1);
-        tile[ty][tx] = blur ? (uint8_t)blur_at(src, rpitch, step, H, W, y, x)
-                            : src[(size_t)y * rpitch + (size_t)x * step];
+    const int t = tid_x();
+    if (blur) {
+        // real rows/columns the clamped window touches, and the raw pixels
+        // (one further, reflected) their 3x3 blur reads
+        const int ylo = y0 - HH > 0 ? y0 - HH : 0, xlo = x0 - HWW > 0 ? x0 - HWW : 0;
+        uint8_t v[RAW_IT];
+#pragma unroll
+        for (int u = 0; u < RAW_IT; ++u) {
+            const int idx = u * 256 + t;
+            const int ry = idx / RC, rx = idx - ry * RC;
+            const int y = reflect101(clampi(ylo - 1 + ry, -1, H), H);
+            const int x = reflect101(clampi(xlo - 1 + rx, -1, W), W);
+            v[u] = idx < RR * RC ? src[(size_t)y * rpitch + (size_t)x * step] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < RAW_IT; ++u) {
+            const int idx = u * 256 + t;
+            if (idx < RR * RC) (&raw[0][0])[idx] = v[u];
+        }
+        __syncthreads();
+        for (int idx = t; idx < TR * TC; idx += 256) {
+            const int ty = idx / TC, tx = idx - ty * TC;
+            const int ry = clampi(y0 + ty - HH, 0, H - 1) - ylo;
+            const int rx = clampi(x0 + tx - HWW, 0, W - 1) - xlo;
+            constexpr int ky[3] = {70, 116, 70};
+            int acc = 0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const uint8_t *row = &raw[ry + r][rx];
+                acc += ky[r] * (82 * row[0] + 93 * row[1] + 82 * row[2]);
+            }
+            const int b = (acc + (1 << 15)) >> 16;  // Pinned blur: see blur_at
+            tile[ty][tx] = (uint8_t)(b > 255 ? 255 : b);
+        }
+    } else {
+        for (int idx = t; idx < TR * TC; idx += 256) {
+            const int ty = idx / TC, tx = idx - ty * TC;
+            const int y = clampi(y0 + ty - HH, 0, H - 1), x = clampi(x0 + tx - HWW, 0, W - 1);
+            tile[ty][tx] = src[(size_t)y * rpitch + (size_t)x * step];
+        }
     }
     __syncthreads();
-    const int tx = tid_x() & 63;
-    for (int r = wave_id(); r < CT_TH; r += 4) {
-        const int y = y0 + r, x = x0 + tx;
-        if (y >= H || x >= W) continue;
-        const uint8_t c = tile[r + HH][tx + HWW];
-        uint64_t v = 0;
+    const int tx = t & 63, r0 = wave_id() * CT_RPT;
+    constexpr int NB = (2 * HH + 1) * (2 * HWW + 1) - 1;  // census bits (62 at 7x9)
+    static_assert(NB <= 64, "census word");
+    constexpr int NHI = NB > 32 ? NB - 32 : 0;            // bits in the high word
+    int c[CT_RPT];
 #pragma unroll
-        for (int di = -HH; di <= HH; ++di)
+    for (int p = 0; p < CT_RPT; ++p) c[p] = tile[r0 + p + HH][tx + HWW];
+    unsigned hi[CT_RPT], lo[CT_RPT];
 #pragma unroll
-            for (int dj = -HWW; dj <= HWW; ++dj) {
-                if (di == 0 && dj == 0) continue;
-                v = (v << 1) | (uint64_t)(tile[r + HH + di][tx + HWW + dj] > c);
+    for (int p = 0; p < CT_RPT; ++p) hi[p] = lo[p] = 0;
+    // window row rr (tile row r0 + rr) is row di = rr - HH - p of pixel p
+#pragma unroll
+    for (int rr = 0; rr < CT_RPT + 2 * HH; ++rr) {
+        int b[2 * HWW + 1];
+#pragma unroll
+        for (int dj = 0; dj <= 2 * HWW; ++dj) b[dj] = tile[r0 + rr][tx + dj];
+#pragma unroll
+        for (int p = 0; p < CT_RPT; ++p) {
+            const int di = rr - p;  // 0 .. 2HH within the window
+            if (di < 0 || di > 2 * HH) continue;
+#pragma unroll
+            for (int dj = 0; dj <= 2 * HWW; ++dj) {
+                if (di == HH && dj == HWW) continue;
+                // bit position k (0 = first, MSB) of the reference's order
+                const int k = di * (2 * HWW + 1) + dj - (di * (2 * HWW + 1) + dj > HH * (2 * HWW + 1) + HWW ? 1 : 0);
+                const unsigned bit = b[dj] > c[p] ? 1u : 0u;
+                if (k < NHI) hi[p] = (hi[p] << 1) | bit;
+                else lo[p] = (lo[p] << 1) | bit;
             }
-        ct[(size_t)y * W + x] = v;
+        }
+    }
+    const int x = x0 + tx;
+#pragma unroll
+    for (int p = 0; p < CT_RPT; ++p) {
+        const int y = y0 + r0 + p;
+        if (y < H && x < W) ct[(size_t)y * W + x] = ((uint64_t)hi[p] << 32) | lo[p];
     }
 }
 
