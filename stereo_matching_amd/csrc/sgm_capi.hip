@@ -315,12 +315,18 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
 // build_dsi_from_table[_beta] (dsi 0 / 1) + horizontal IIR (cost_h), then
 // the vertical IIR fused with the L3 forward pass (vfwd), into view slot
 // `view`'s buffers.
+int vfwd_view(sgm_handle *h, int view, hipStream_t st);
 int cost_view(sgm_handle *h, int view, int dsi, const uint8_t *sky, int sky_pitch, hipStream_t st) {
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     HIPCHK(h, timed(h, "cost_h", elems, st, [&] {
                return sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky, sky_pitch, dsi, 1, h->g,
                                          h->d_ch[view], st);
            }));
+    return vfwd_view(h, view, st);
+}
+
+int vfwd_view(sgm_handle *h, int view, hipStream_t st) {
+    const double elems = (double)h->g.H * h->g.W * h->g.D;
     sgm::PairArgs pa = pair_args(h);
     pa.ckpt = h->d_ck[view][sgm::PAIR_V];
     HIPCHK(h, timed(h, "vfwd", elems, st, [&] {
@@ -397,14 +403,27 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                                          d_right, h->d_ct[1]);
            }));
     HIPCHK(h, hipEventRecord(h->ev_ct, st));
-    if (h->nviews == 2) {
-        HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
-        if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
-        HIPCHK(h, hipEventRecord(h->ev_c[1], aux1));
+    // two views on one stream: both DSIs + horizontal IIRs in one launch (a
+    // view's H*D serial chains alone leave most SIMDs idle at KITTI sizes)
+    const bool both_h = h->nviews == 2 && aux1 == st && (d_sky_l == nullptr) == (d_sky_r == nullptr) &&
+                        sgm::cost_h2_supported(g, d_sky_l != nullptr);
+    if (both_h) {
+        HIPCHK(h, timed(h, "cost_h", 2.0 * npx * g.D, st, [&] {
+                   return sgm::launch_cost_h2(h->d_ct[0], h->d_ct[1], d_sky_l, d_sky_r, sky_pitch, g,
+                                              h->d_ch[0], h->d_ch[1], st);
+               }));
+        if ((rc = vfwd_view(h, 1, st)) != SGM_OK) return rc;
+        if ((rc = vfwd_view(h, 0, st)) != SGM_OK) return rc;
+    } else {
+        if (h->nviews == 2) {
+            HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
+            if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
+            HIPCHK(h, hipEventRecord(h->ev_c[1], aux1));
+        }
+        if ((rc = cost_view(h, 0, right_only ? 1 : 0, right_only ? d_sky_r : d_sky_l, sky_pitch,
+                            st)) != SGM_OK)
+            return rc;
     }
-    if ((rc = cost_view(h, 0, right_only ? 1 : 0, right_only ? d_sky_r : d_sky_l, sky_pitch, st)) !=
-        SGM_OK)
-        return rc;
     HIPCHK(h, hipEventRecord(h->ev_c[0], st));
     if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
                              false)) != SGM_OK)

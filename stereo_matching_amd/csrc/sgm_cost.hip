@@ -192,18 +192,17 @@ __host__ __device__ constexpr int costh_pad(int D, int scale) { return D / scale
 // scalar load from global memory; only the per-lane shifted row is staged in
 // LDS, which halves the staging and keeps 4K rows (3840 px) inside 64 KiB.
 template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI>
-__global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
-                                                     const uint64_t *__restrict__ ctr,
-                                                     const uint8_t *__restrict__ sky,
-                                                     int sky_pitch, int H, int W, int D, int scale,
-                                                     int R, float *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
+                                            const uint64_t *__restrict__ ctr,
+                                            const uint8_t *__restrict__ sky, int sky_pitch, int H,
+                                            int W, int D, int scale, int R,
+                                            float *__restrict__ out, int blk, unsigned char *smem) {
     const int P = costh_pad(D, scale), RS = W + 2 * P;
     constexpr int NS = UNI ? 1 : 2;  // staged census rows per image row
     uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
     uint64_t *sr = sl + (UNI ? 0 : (size_t)R * RS);
     uint8_t *ss = reinterpret_cast<uint8_t *>(sl + (size_t)NS * R * RS);
-    const int row0 = bid_x() * R;
+    const int row0 = blk * R;
     for (int idx = tid_x(); idx < R * RS; idx += R * D) {
         const int r = idx / RS, jp = idx - r * RS, i = row0 + r;
         const int j = clampi(jp - P, 0, W - 1);
@@ -306,6 +305,38 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
     for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
 }
 
+template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI>
+__global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
+                                                     const uint64_t *__restrict__ ctr,
+                                                     const uint8_t *__restrict__ sky,
+                                                     int sky_pitch, int H, int W, int D, int scale,
+                                                     int R, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cost_h_body<VIEW, WIN, SKY, FILTER, UNI>(ctl, ctr, sky, sky_pitch, H, W, D, scale, R, out,
+                                             bid_x(), smem);
+}
+
+// Both views in one launch (workgroup z = view): the DSI of
+// build_dsi_from_table into out0 and of build_dsi_from_table_beta into out1,
+// each with its own sky mask.  A view's H*D chains fill less than the chip at
+// KITTI sizes, so the two views' chains run side by side.
+template <int WIN, bool SKY, bool FILTER, bool UNI>
+__global__ __launch_bounds__(256) void cost_h2_kernel(const uint64_t *__restrict__ ctl,
+                                                      const uint64_t *__restrict__ ctr,
+                                                      const uint8_t *__restrict__ sky0,
+                                                      const uint8_t *__restrict__ sky1,
+                                                      int sky_pitch, int H, int W, int D, int scale,
+                                                      int R, float *__restrict__ out0,
+                                                      float *__restrict__ out1) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (__builtin_amdgcn_workgroup_id_z() == 0)
+        cost_h_body<0, WIN, SKY, FILTER, UNI>(ctl, ctr, sky0, sky_pitch, H, W, D, scale, R, out0,
+                                              bid_x(), smem);
+    else
+        cost_h_body<1, WIN, SKY, FILTER, UNI>(ctl, ctr, sky1, sky_pitch, H, W, D, scale, R, out1,
+                                              bid_x(), smem);
+}
+
 // Fallback for rows too wide to stage in LDS (W*16 B > 64 KiB): census words
 // read straight from global memory.
 template <int VIEW, int WIN, bool SKY, bool FILTER>
@@ -357,19 +388,28 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
     for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
 }
 
+// rows per block and LDS bytes of the staged cost_h_kernel (R = 0: the
+// global-memory fallback)
+static void costh_shape(Geom g, bool sky, bool &uni, int &R, size_t &smem) {
+    const size_t rs = (size_t)(g.W + 2 * costh_pad(g.D, g.scale));
+    uni = g.D >= 64 && rs * (16 + (sky ? 1 : 0)) > (size_t)COSTH_MAX_LDS;
+    const size_t row_bytes = rs * ((uni ? 8 : 16) + (sky ? 1 : 0));
+    R = (int)(COSTH_MAX_LDS / row_bytes);
+    if (R > 256 / g.D) R = 256 / g.D;
+    smem = (size_t)(R > 0 ? R : 0) * row_bytes;
+}
+
 template <int VIEW, int WIN, bool SKY, bool FILTER>
 static void launch_cost_h_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                             int sky_pitch, Geom g, float *out, hipStream_t st) {
     // stage both census rows when they fit (faster: LDS reads for both
     // operands); rows too wide for that (4K) stage one and load the uniform
     // operand as scalars
-    const size_t rs = (size_t)(g.W + 2 * costh_pad(g.D, g.scale));
-    const bool uni = g.D >= 64 && rs * (16 + (SKY ? 1 : 0)) > (size_t)COSTH_MAX_LDS;
-    const size_t row_bytes = rs * ((uni ? 8 : 16) + (SKY ? 1 : 0));
-    int R = (int)(COSTH_MAX_LDS / row_bytes);
-    if (R > 256 / g.D) R = 256 / g.D;
+    bool uni;
+    int R;
+    size_t smem;
+    costh_shape(g, SKY, uni, R, smem);
     if (R >= 1) {
-        const size_t smem = (size_t)R * row_bytes;
         if (uni)
             cost_h_kernel<VIEW, WIN, SKY, FILTER, true><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
                 ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
@@ -393,6 +433,45 @@ static void launch_cost_h_w(const uint64_t *ctl, const uint64_t *ctr, const uint
         if (filter) launch_cost_h_t<VIEW, WIN, false, true>(ctl, ctr, sky, sky_pitch, g, out, st);
         else launch_cost_h_t<VIEW, WIN, false, false>(ctl, ctr, sky, sky_pitch, g, out, st);
     }
+}
+
+template <int WIN, bool SKY, bool FILTER>
+static hipError_t launch_cost_h2_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky0,
+                                   const uint8_t *sky1, int sky_pitch, Geom g, float *out0,
+                                   float *out1, hipStream_t st) {
+    bool uni;
+    int R;
+    size_t smem;
+    costh_shape(g, SKY, uni, R, smem);
+    if (R < 1) return hipErrorInvalidValue;  // the caller launches the views one by one
+    const dim3 grid((g.H + R - 1) / R, 1, 2);
+    if (uni)
+        cost_h2_kernel<WIN, SKY, FILTER, true><<<grid, R * g.D, smem, st>>>(
+            ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, g.scale, R, out0, out1);
+    else
+        cost_h2_kernel<WIN, SKY, FILTER, false><<<grid, R * g.D, smem, st>>>(
+            ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, g.scale, R, out0, out1);
+    return hipGetLastError();
+}
+
+bool cost_h2_supported(Geom g, bool sky) {
+    bool uni;
+    int R;
+    size_t smem;
+    costh_shape(g, sky, uni, R, smem);
+    return R >= 1;
+}
+
+hipError_t launch_cost_h2(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky0,
+                          const uint8_t *sky1, int sky_pitch, Geom g, float *out0, float *out1,
+                          hipStream_t st) {
+    if ((sky0 == nullptr) != (sky1 == nullptr)) return hipErrorInvalidValue;
+    if (sky0) {
+        if (g.scale == 1) return launch_cost_h2_t<5, true, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
+        return launch_cost_h2_t<2, true, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
+    }
+    if (g.scale == 1) return launch_cost_h2_t<5, false, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
+    return launch_cost_h2_t<2, false, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
 }
 
 hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,

@@ -86,6 +86,12 @@ hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64
 // BM's WTA (BM.cpp:53-85) over the filtered cost: raw disparity + its float copy
 hipError_t launch_bm_wta(const float *cost, float uniq, uint16_t *disp, float *out, int out_pitch,
                          Geom g, hipStream_t st);
+// both views' DSI + horizontal IIR in one launch (both sky masks or neither);
+// cost_h2_supported: false when rows do not fit the staged kernel
+bool cost_h2_supported(Geom g, bool sky);
+hipError_t launch_cost_h2(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky0,
+                          const uint8_t *sky1, int sky_pitch, Geom g, float *out0, float *out1,
+                          hipStream_t st);
 hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                          int sky_pitch, int view, int filter, Geom g, float *out,
                          hipStream_t st);
