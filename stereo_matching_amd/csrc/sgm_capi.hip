@@ -275,7 +275,7 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
 // (the reference's order, SGM.cpp:386-390).  T may alias the dead
 // horizontally filtered volume.
 int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *T, uint16_t *disp,
-                   float *sub, hipStream_t st, bool need_v_ckpt) {
+                   float *sub, hipStream_t st, bool need_v_ckpt, sgm::PairArgs *defer_final = nullptr) {
     float **ck = h->d_ck[view];
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     sgm::PairArgs pa = pair_args(h);
@@ -308,6 +308,10 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     pa.acc_in = T;
     pa.disp = disp;
     pa.sub = sub;
+    if (defer_final) {  // the caller launches this view's final pass with the other view's
+        *defer_final = pa;
+        return SGM_OK;
+    }
     HIPCHK(h, pair_bwd(h, sgm::PAIR_V, sgm::PAIR_FINAL, pa, st));
     return SGM_OK;
 }
@@ -425,13 +429,23 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
             return rc;
     }
     HIPCHK(h, hipEventRecord(h->ev_c[0], st));
+    // Volumes larger than the 256 MB Infinity Cache gain nothing from
+    // finishing the left view first: both views' final passes then run as one
+    // launch (fewer workgroup rounds at HD/4K)
+    const bool both_final = h->nviews == 2 && aux1 == st &&
+                            (double)g.H * g.W * g.D * sizeof(float) > 256.0 * 1024 * 1024 &&
+                            !getenv("SGM_SPLIT_FINAL");
+    sgm::PairArgs fin[2];
     if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
-                             false)) != SGM_OK)
+                             false, both_final ? &fin[0] : nullptr)) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
         if ((rc = aggregate_view(h, 1, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
-                                 aux1, false)) != SGM_OK)
+                                 aux1, false, both_final ? &fin[1] : nullptr)) != SGM_OK)
             return rc;
+        if (both_final)
+            HIPCHK(h, timed(h, "pair_bwd_L4_final", 2.0 * npx * g.D, st,
+                            [&] { return sgm::launch_final2(fin[0], fin[1], g, st); }));
         HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
         HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
         HIPCHK(h, timed(h, "lr", npx, st, [&] {

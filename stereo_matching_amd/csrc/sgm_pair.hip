@@ -157,6 +157,20 @@ __global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {
         a, g, bid_x(), wave_id(), lds.s, &lds);
 }
 
+// Both views' final passes in one launch (workgroup z = view).  Above the
+// Infinity Cache nothing is gained by finishing a view before the other one
+// starts, and one launch of 2W columns packs the workgroups into fewer rounds
+// (HD256: 2 x 1920 columns at 1280 resident workgroups take 3 rounds instead
+// of 2 + 2).
+template <int V, bool FULL>
+__global__ __launch_bounds__(256) void pair_final2_kernel(PairArgs a0, PairArgs a1, Geom g) {
+    constexpr int K = pair_kv<V>();
+    __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
+    const PairArgs &a = __builtin_amdgcn_workgroup_id_z() != 0 ? a1 : a0;
+    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>()>(
+        a, g, bid_x(), wave_id(), lds.s, &lds);
+}
+
 // Multi-role stage kernels of the frame schedule: block ranges run different
 // (independent) roles, so a latency-bound horizontal role (H chains, few and
 // long) overlaps the bandwidth-bound diagonal roles inside one launch.  The
@@ -268,6 +282,15 @@ static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
     else if (g.D == 64) pair_final_kernel<1, true><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a, g);
     else if (g.D == 128) pair_final_kernel<2, true><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a, g);
     else pair_final_kernel<4, true><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a, g);
+}
+
+hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStream_t st) {
+    const dim3 grid(g.W, 1, 2);
+    if (g.D == 32) pair_final2_kernel<1, false><<<grid, 64 * (2 + final_nwta<1, false>()), 0, st>>>(a0, a1, g);
+    else if (g.D == 64) pair_final2_kernel<1, true><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a0, a1, g);
+    else if (g.D == 128) pair_final2_kernel<2, true><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a0, a1, g);
+    else pair_final2_kernel<4, true><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a0, a1, g);
+    return hipGetLastError();
 }
 
 hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipStream_t st) {
