@@ -436,8 +436,12 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                             (double)g.H * g.W * g.D * sizeof(float) > 256.0 * 1024 * 1024 &&
                             !getenv("SGM_SPLIT_FINAL");
     sgm::PairArgs fin[2];
-    if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0], st,
-                             false, both_final ? &fin[0] : nullptr)) != SGM_OK)
+    // one view with a dense output map: the final pass writes the sub-pixel
+    // map straight into it (no device copy after the frame)
+    const bool direct_out = h->nviews == 1 && out_pitch == g.W;
+    if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0],
+                             direct_out ? d_out : h->d_sub[0], st, false,
+                             both_final ? &fin[0] : nullptr)) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
         if ((rc = aggregate_view(h, 1, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
@@ -452,7 +456,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                    return sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
                                          h->p.lr_max_diff, g, st);
                }));
-    } else {
+    } else if (!direct_out) {
         HIPCHK(h, hipMemcpy2DAsync(d_out, (size_t)out_pitch * sizeof(float), h->d_sub[0],
                                    (size_t)g.W * sizeof(float), (size_t)g.W * sizeof(float), g.H,
                                    hipMemcpyDeviceToDevice, st));
