@@ -30,23 +30,9 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i >= n ? 2 * n - 2 - i : i;
 }
 
-// rpitch: bytes between working-grid rows (step * pitch for SGM.cpp:47-48's
-// decimation, pitch for BM.cpp:24-25's); step: pixels between columns.
-__device__ __forceinline__ int blur_at(const uint8_t *src, int rpitch, int step, int H, int W,
-                                       int y, int x) {
-    const int xm = reflect101(x - 1, W) * step, x0 = x * step, xp = reflect101(x + 1, W) * step;
-    const int ys[3] = {reflect101(y - 1, H), y, reflect101(y + 1, H)};
-    const int ky[3] = {70, 116, 70};
-    int acc = 0;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const uint8_t *row = src + (size_t)ys[r] * rpitch;
-        acc += ky[r] * (82 * row[xm] + 93 * row[x0] + 82 * row[xp]);
-    }
-    const int v = (acc + (1 << 15)) >> 16;
-    return v > 255 ? 255 : v;
-}
-
+// Census inputs: rpitch = bytes between working-grid rows (step * pitch for
+// SGM.cpp:47-48's decimation, pitch for BM.cpp:24-25's); step = pixels
+// between columns.
 constexpr int CT_TW = 64, CT_TH = 16, CT_RPT = CT_TH / 4;  // 4 waves x CT_RPT rows
 
 // CT_pts (cost.cpp:99-129) for one image; window (2HH+1) x (2HWW+1) = 7x9 (3x5
@@ -105,7 +91,7 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
                 const uint8_t *row = &raw[ry + r][rx];
                 acc += ky[r] * (82 * row[0] + 93 * row[1] + 82 * row[2]);
             }
-            const int b = (acc + (1 << 15)) >> 16;  // Pinned blur: see blur_at
+            const int b = (acc + (1 << 15)) >> 16;  // the pinned blur (top of file)
             tile[ty][tx] = (uint8_t)(b > 255 ? 255 : b);
         }
     } else {
