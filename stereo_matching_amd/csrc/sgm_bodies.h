@@ -54,6 +54,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 #ifdef SGM_STAMPS
     const long long st_t0 = __builtin_amdgcn_s_memtime();
 #endif
+    const float p2v = to_vgpr(a.p2);  // dp_step's P2 operand
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -89,7 +90,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
             ai[v] = ab[u][v];
         }
         float L[V];
-        dp_step<V>(prev, pmin, c, L, a.p1, a.p2);
+        dp_step<V>(prev, pmin, c, L, a.p1, p2v);
         const bool st = cc.start(W);
 #pragma unroll
         for (int v = 0; v < V; ++v) L[v] = st ? c[v] : L[v];
@@ -161,6 +162,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     constexpr int K = family_k<FD == 0 ? PAIR_H : (FD == 2 ? PAIR_V : PAIR_D2), V>();
     static_assert(PF % K == 0, "the ring covers whole checkpoint segments");
     constexpr bool DIAG = FD == 5;
+    const float p2v = to_vgpr(a.p2);  // dp_step's P2 operand
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -219,7 +221,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
 
     auto step = [&](int u, bool refill) {
         float L[V];
-        dp_step<V>(prev, pmin, cb[u], L, a.p1, a.p2);
+        dp_step<V>(prev, pmin, cb[u], L, a.p1, p2v);
         if constexpr (DIAG) {
             // a wrapped diagonal restarts where it meets the image edge
             const bool st = cpos > 0 && cc.start(W);
@@ -267,6 +269,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     constexpr bool NEED_ACC = MODE != PAIR_INIT2;
     constexpr bool NEED_S = FINAL;
     const int wave = wave_id();
+    const float p2v = to_vgpr(a.p2);  // dp_step's P2 operand
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -350,7 +353,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
         for (int kk = 0; kk < K; ++kk) {
             if (FULLSEG || kk >= skip) {
                 float L[V];
-                dp_step<V>(pf, pminf, cs[kk], L, a.p1, a.p2);
+                dp_step<V>(pf, pminf, cs[kk], L, a.p1, p2v);
                 const bool st = fc.start(W);
 #pragma unroll
                 for (int v = 0; v < V; ++v) L[v] = st ? cs[kk][v] : L[v];
@@ -370,7 +373,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
             const int kk = K - 1 - r;
             if (FULLSEG || kk >= skip) {
                 float L[V];
-                dp_step<V>(prevb, pminb, cs[kk], L, a.p1, a.p2);
+                dp_step<V>(prevb, pminb, cs[kk], L, a.p1, p2v);
                 const bool st = bc.start(W);
 #pragma unroll
                 for (int v = 0; v < V; ++v) L[v] = st ? cs[kk][v] : L[v];
@@ -489,6 +492,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     // keeps one stream in flight
     constexpr bool NEED_ACC = MODE == PAIR_ACC;
     constexpr bool NEED_S = FINAL;
+    const float p2v = to_vgpr(a.p2);  // dp_step's P2 operand
     const int lane = tid_x() & 63;
     const int H = g.H, W = g.W;
     const long long D = g.D, WD = (long long)g.W * g.D;
@@ -564,7 +568,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             for (int kk = 0; kk < K; ++kk) {
                 if (FULLSEG || kk >= skip) {
                     float Lr[V];
-                    dp_step<V>(pf, pminf, cs[kk], Lr, a.p1, a.p2);
+                    dp_step<V>(pf, pminf, cs[kk], Lr, a.p1, p2v);
                     if constexpr (!LIN) {
                         const bool st = fc.start(W);
 #pragma unroll
@@ -661,7 +665,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     load_lds_v<V>(cs, &L.c[buf][kk][e0]);
                     load_lds_v<V>(lf, &L.l[buf][kk][e0]);
                     float Lr[V];
-                    dp_step<V>(prevb, pminb, cs, Lr, a.p1, a.p2);
+                    dp_step<V>(prevb, pminb, cs, Lr, a.p1, p2v);
                     if constexpr (!LIN) {
                         const bool st = bc.start(W);
 #pragma unroll

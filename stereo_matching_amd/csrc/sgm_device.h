@@ -109,6 +109,23 @@ __device__ __forceinline__ float nbmin(float src, float a) {
     return d;
 }
 
+// A uniform value copied into a VGPR (once, outside a chain's loop).
+__device__ __forceinline__ float to_vgpr(float x) {
+    float v;
+    asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+
+// min(x of the neighbouring lane, x) in place (the edge lane keeps x)
+template <int CTRL>
+__device__ __forceinline__ float nbmin_self(float x) {
+    if constexpr (CTRL == DPP_WAVE_SHR1)
+        asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(x));
+    else
+        asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 wave_shl:1 row_mask:0xf bank_mask:0xf" : "+v"(x));
+    return x;
+}
+
 __device__ __forceinline__ int wave_min_i(int x) {
     x = min(x, movdpp<DPP_QP_1032>(x));
     x = min(x, movdpp<DPP_QP_2301>(x));
@@ -299,32 +316,47 @@ __device__ __forceinline__ void store_v(float *p, const float (&v)[V], bool acti
 template <int V>
 __device__ __forceinline__ void dp_step(const float (&prev)[V], float pmin, const float (&c)[V],
                                         float (&L)[V], float p1, float p2) {
-    // neighbour minima min(L[d-1], L[d+1]); d = lane*V + v
-    float nb[V];
-    if constexpr (V == 1) {
-        const float right = dppf<DPP_WAVE_SHL1>(SGM_INF, prev[0]);
-        nb[0] = nbmin<DPP_WAVE_SHR1>(prev[0], right);
-    } else {
-        nb[0] = nbmin<DPP_WAVE_SHR1>(prev[V - 1], prev[1]);
-#pragma unroll
-        for (int v = 1; v < V - 1; ++v) nb[v] = fminf(prev[v - 1], prev[v + 1]);
-        nb[V - 1] = nbmin<DPP_WAVE_SHL1>(prev[0], prev[V - 2]);
-    }
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    // callers pass P2 as a VGPR (to_vgpr, once per chain): minLp (an SGPR) +
+    // P2 is then one VALU op (a VALU op reads at most one SGPR)
     const float pmin_p2 = pmin + p2;
     if constexpr (V == 1) {
-        const float m = fminf(fminf(prev[0], nb[0] + p1), pmin_p2);
+        // neighbour minima min(L[d-1], L[d+1]) (d = lane)
+        const float right = dppf<DPP_WAVE_SHL1>(SGM_INF, prev[0]);
+        const float nb = nbmin<DPP_WAVE_SHR1>(prev[0], right);
+        const float m = fminf(fminf(prev[0], nb + p1), pmin_p2);
         L[0] = m + (c[0] - pmin);
     } else {
-        // pairs of lanes' values through packed f32 adds (v_pk_add_f32);
-        // same IEEE single additions as the scalar form
-        typedef float f2 __attribute__((ext_vector_type(2)));
+        // q = Lp + P1 first (rounding is monotone, so min(a, b) + P1 ==
+        // min(a + P1, b + P1) bit for bit), then the neighbour minima of q
+        // in place: each q value that feeds a cross-lane minimum is dead
+        // after it, so the DPP op can overwrite it (its edge lane keeps the
+        // in-lane neighbour) and no copies are needed
+        float q[V];
 #pragma unroll
         for (int v = 0; v < V; v += 2) {
-            const f2 t = f2{nb[v], nb[v + 1]} + p1;
+            const f2 t = f2{prev[v], prev[v + 1]} + p1;
+            q[v] = t.x;
+            q[v + 1] = t.y;
+        }
+        float t[V];
+        if constexpr (V == 2) {
+            // t0 = min(q1[l-1], q1), t1 = min(q0, q0[l+1])
+            t[0] = nbmin_self<DPP_WAVE_SHR1>(q[1]);
+            t[1] = nbmin_self<DPP_WAVE_SHL1>(q[0]);
+        } else {
+            // t0 = min(q3[l-1], q1), t1 = min(q0, q2), t2 = min(q1, q3), t3 = min(q2, q0[l+1])
+            t[1] = fminf(q[0], q[2]);
+            t[2] = fminf(q[1], q[3]);
+            t[0] = nbmin<DPP_WAVE_SHR1>(q[3], q[1]);
+            t[3] = nbmin<DPP_WAVE_SHL1>(q[0], q[2]);
+        }
+#pragma unroll
+        for (int v = 0; v < V; v += 2) {
             const f2 d = f2{c[v], c[v + 1]} - pmin;
             f2 m;
-            m.x = fminf(fminf(prev[v], t.x), pmin_p2);
-            m.y = fminf(fminf(prev[v + 1], t.y), pmin_p2);
+            m.x = fminf(fminf(prev[v], t[v]), pmin_p2);
+            m.y = fminf(fminf(prev[v + 1], t[v + 1]), pmin_p2);
             const f2 r = m + d;
             L[v] = r.x;
             L[v + 1] = r.y;

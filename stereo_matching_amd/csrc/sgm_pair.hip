@@ -45,6 +45,7 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     constexpr int K = pair_kv<V>();
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, LA = HALF + 1;
     const int lane = tid_x();
+    const float p2v = to_vgpr(a.p2);  // dp_step's P2 operand
     const int j = bid_x();
     const int H = g.H;
     const size_t stride = (size_t)g.W * g.D;
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
         store_v<V>(ocol + (size_t)i * stride, c, active);
         // L3 forward step on the freshly filtered row
         float L[V];
-        dp_step<V>(prev, pmin, c, L, a.p1, a.p2);
+        dp_step<V>(prev, pmin, c, L, a.p1, p2v);
         const float nmin = wave_min(lane_min(L));
         if (i == next_ck && ck_i < nseg - 1) {
             store_v<V>(ck + (size_t)ck_i * g.D, L, active);
