@@ -215,7 +215,9 @@ struct Cursor {
             const long long di = DIR == 4 ? WD : -WD;
             const bool wrap = j == W - 1;
             off += di + (wrap ? -(long long)(W - 1) * D : D);
-            j = wrap ? 0 : j + 1;
+            // pinned to an SGPR: left alone hipcc carries j in a VGPR and
+            // spends VALU ops on every step's wrap test and select
+            j = uniform(wrap ? 0 : j + 1);
             i += DIR == 4 ? 1 : -1;
             break;
         }
@@ -223,7 +225,7 @@ struct Cursor {
             const long long di = DIR == 5 ? WD : -WD;
             const bool wrap = j == 0;
             off += di + (wrap ? (long long)(W - 1) * D : -D);
-            j = wrap ? W - 1 : j - 1;
+            j = uniform(wrap ? W - 1 : j - 1);
             i += DIR == 5 ? 1 : -1;
             break;
         }
