@@ -1,14 +1,17 @@
-// sgm_cost.hip -- census, DSI + horizontal IIR, vertical IIR.
+// sgm_cost.hip -- census, DSI + horizontal IIR (the vertical IIR runs fused
+// with the L3 forward pass in sgm_pair.hip).
 // CDNA4 (gfx950) kernels of the semi-global matcher.
 //
 // Stage map (reference -> kernel), full design in DESIGN.md:
 //   cv::GaussianBlur + CT_pts     Solver.cpp:120-140, cost.cpp:99-129  -> census_kernel
 //   build_dsi_from_table[_beta]   Solver.cpp:143-248
-//     + cost_horizontal_filter    Solver.cpp:296-330                   -> cost_h_kernel
-//   cost_vertical_filter          Solver.cpp:333-368                   -> cost_v_kernel
-//   L1..L8 path DP                SGM.cpp:81-369                       -> sweep_kernel<DIR,..>
+//     + cost_horizontal_filter    Solver.cpp:296-330                   -> cost_h_kernel,
+//                                                                         cost_h2_kernel (both views)
+//   cost_vertical_filter          Solver.cpp:333-368                   -> vfwd_kernel (sgm_pair.hip)
+//   L1..L8 path DP                SGM.cpp:81-369                       -> stage_a/stage_b kernels,
+//                                                                         sweep_kernel (sgm_sweep.hip)
 //   aggregation + WTA + unique    SGM.cpp:372-418
-//     + compute_subpixel          Solver.cpp:569-597                   -> sweep_kernel<..,FINAL>
+//     + compute_subpixel          Solver.cpp:569-597                   -> pair_final_kernel
 //   LR check                      SGM.cpp:803-818                      -> lr_kernel
 //
 // Bit-exactness rules (DESIGN.md "Numerics"): built with -ffp-contract=off,

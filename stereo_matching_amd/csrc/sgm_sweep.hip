@@ -1,11 +1,12 @@
-// sgm_sweep.hip -- single-direction path sweeps, the fused final sweep, LR check.
+// sgm_sweep.hip -- single-direction path sweeps (the production L8 pass and
+// the per-direction parity stages), LR check.
 // CDNA4 (gfx950) kernels of the semi-global matcher.
 //
 // Stage map (reference -> kernel), full design in DESIGN.md:
 //   cv::GaussianBlur + CT_pts     Solver.cpp:120-140, cost.cpp:99-129  -> census_kernel
 //   build_dsi_from_table[_beta]   Solver.cpp:143-248
 //     + cost_horizontal_filter    Solver.cpp:296-330                   -> cost_h_kernel
-//   cost_vertical_filter          Solver.cpp:333-368                   -> cost_v_kernel
+//   cost_vertical_filter          Solver.cpp:333-368                   -> vfwd_kernel
 //   L1..L8 path DP                SGM.cpp:81-369                       -> sweep_kernel<DIR,..>
 //                                                     (pairs: sgm_pair.hip)
 //   aggregation + WTA + unique    SGM.cpp:372-418
