@@ -180,7 +180,9 @@ __host__ __device__ constexpr int costh_pad(int D, int scale) { return D / scale
 // at step j -- cl[j] for the left view, cr[j] for the right -- is a uniform
 // scalar load from global memory; only the per-lane shifted row is staged in
 // LDS, which halves the staging and keeps 4K rows (3840 px) inside 64 KiB.
-template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI>
+// DC: D as a compile-time constant (0: runtime D), so the stores of an
+// unrolled block take immediate offsets instead of a 64-bit address add each
+template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI, int DC = 0>
 __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
                                             const uint64_t *__restrict__ ctr,
                                             const uint8_t *__restrict__ sky, int sky_pitch, int H,
@@ -212,6 +214,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     const uint64_t *cu = (VIEW == 0 ? ctl : ctr) + (size_t)i * W;  // UNI: the uniform row
     const uint8_t *sk = ss + (size_t)r * RS + P;
     float *o = out + (size_t)i * W * D + d;
+    const size_t DS = DC ? (size_t)DC : (size_t)D;  // store stride
 
     auto word_l = [&](int j) { return UNI && VIEW == 0 ? cu[j < W - 1 ? j : W - 1] : cl[j]; };
     auto word_r = [&](int j) { return UNI && VIEW == 1 ? cu[j < W - 1 ? j : W - 1] : cr[j]; };
@@ -226,7 +229,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     };
 
     if (!FILTER) {
-        for (int j = 0; j < W; ++j) __builtin_nontemporal_store(raw(j), o + (size_t)j * D);
+        for (int j = 0; j < W; ++j) __builtin_nontemporal_store(raw(j), o + (size_t)j * DS);
         return;
     }
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, U = COSTH_U;
@@ -234,7 +237,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
 #pragma unroll
-    for (int p = 0; p < LAG; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
+    for (int p = 0; p < LAG; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * DS);
     const int T = W - 2 * HALF;
     // hist[0] is what step t subtracts: raw[t] for t < LAG, output t-LAG after
     float hist[LAG > 0 ? LAG : 1];
@@ -242,7 +245,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     for (int p = 0; p < LAG; ++p) hist[p] = raw(p);
     auto step = [&](int t, float rw) {
         const float v = div_win<WIN>(sum);
-        __builtin_nontemporal_store(v, o + (size_t)(LAG + t) * D);
+        __builtin_nontemporal_store(v, o + (size_t)(LAG + t) * DS);
         sum += rw;
         float a;
         if constexpr (LAG == 0) {
@@ -290,18 +293,18 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
         t += U;
     }
     for (; t < T - 1; ++t) step(t, raw(WIN + t));
-    if (T >= 1) __builtin_nontemporal_store(div_win<WIN>(sum), o + (size_t)(LAG + T - 1) * D);
-    for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
+    if (T >= 1) __builtin_nontemporal_store(div_win<WIN>(sum), o + (size_t)(LAG + T - 1) * DS);
+    for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * DS);
 }
 
-template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI>
+template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI, int DC>
 __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict__ ctl,
                                                      const uint64_t *__restrict__ ctr,
                                                      const uint8_t *__restrict__ sky,
                                                      int sky_pitch, int H, int W, int D, int scale,
                                                      int R, float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    cost_h_body<VIEW, WIN, SKY, FILTER, UNI>(ctl, ctr, sky, sky_pitch, H, W, D, scale, R, out,
+    cost_h_body<VIEW, WIN, SKY, FILTER, UNI, DC>(ctl, ctr, sky, sky_pitch, H, W, D, scale, R, out,
                                              bid_x(), smem);
 }
 
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(256) void cost_h_kernel(const uint64_t *__restrict_
 // build_dsi_from_table into out0 and of build_dsi_from_table_beta into out1,
 // each with its own sky mask.  A view's H*D chains fill less than the chip at
 // KITTI sizes, so the two views' chains run side by side.
-template <int WIN, bool SKY, bool FILTER, bool UNI>
+template <int WIN, bool SKY, bool FILTER, bool UNI, int DC>
 __global__ __launch_bounds__(256) void cost_h2_kernel(const uint64_t *__restrict__ ctl,
                                                       const uint64_t *__restrict__ ctr,
                                                       const uint8_t *__restrict__ sky0,
@@ -319,10 +322,10 @@ __global__ __launch_bounds__(256) void cost_h2_kernel(const uint64_t *__restrict
                                                       float *__restrict__ out1) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if (__builtin_amdgcn_workgroup_id_z() == 0)
-        cost_h_body<0, WIN, SKY, FILTER, UNI>(ctl, ctr, sky0, sky_pitch, H, W, D, scale, R, out0,
+        cost_h_body<0, WIN, SKY, FILTER, UNI, DC>(ctl, ctr, sky0, sky_pitch, H, W, D, scale, R, out0,
                                               bid_x(), smem);
     else
-        cost_h_body<1, WIN, SKY, FILTER, UNI>(ctl, ctr, sky1, sky_pitch, H, W, D, scale, R, out1,
+        cost_h_body<1, WIN, SKY, FILTER, UNI, DC>(ctl, ctr, sky1, sky_pitch, H, W, D, scale, R, out1,
                                               bid_x(), smem);
 }
 
@@ -400,10 +403,13 @@ static void launch_cost_h_t(const uint64_t *ctl, const uint64_t *ctr, const uint
     costh_shape(g, SKY, uni, R, smem);
     if (R >= 1) {
         if (uni)
-            cost_h_kernel<VIEW, WIN, SKY, FILTER, true><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+            cost_h_kernel<VIEW, WIN, SKY, FILTER, true, 0><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+                ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
+        else if (g.D == 128)
+            cost_h_kernel<VIEW, WIN, SKY, FILTER, false, 128><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
                 ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
         else
-            cost_h_kernel<VIEW, WIN, SKY, FILTER, false><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
+            cost_h_kernel<VIEW, WIN, SKY, FILTER, false, 0><<<dim3((g.H + R - 1) / R), R * g.D, smem, st>>>(
                 ctl, ctr, sky, sky_pitch, g.H, g.W, g.D, g.scale, R, out);
     } else {
         const int rpb = 256 / g.D;
@@ -435,10 +441,13 @@ static hipError_t launch_cost_h2_t(const uint64_t *ctl, const uint64_t *ctr, con
     if (R < 1) return hipErrorInvalidValue;  // the caller launches the views one by one
     const dim3 grid((g.H + R - 1) / R, 1, 2);
     if (uni)
-        cost_h2_kernel<WIN, SKY, FILTER, true><<<grid, R * g.D, smem, st>>>(
+        cost_h2_kernel<WIN, SKY, FILTER, true, 0><<<grid, R * g.D, smem, st>>>(
+            ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, g.scale, R, out0, out1);
+    else if (g.D == 128)
+        cost_h2_kernel<WIN, SKY, FILTER, false, 128><<<grid, R * g.D, smem, st>>>(
             ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, g.scale, R, out0, out1);
     else
-        cost_h2_kernel<WIN, SKY, FILTER, false><<<grid, R * g.D, smem, st>>>(
+        cost_h2_kernel<WIN, SKY, FILTER, false, 0><<<grid, R * g.D, smem, st>>>(
             ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, g.scale, R, out0, out1);
     return hipGetLastError();
 }
