@@ -82,9 +82,10 @@ public:
     bool empty() const { return data == nullptr || rows == 0 || cols == 0; }
     int type() const { return type_; }
     int channels() const { return type_ == CV_8UC3 ? 3 : 1; }
-    Mat clone() const {
+    Mat clone() const {  // packed copy (step = cols * elem), row by row as cv::Mat::clone
         Mat m(rows, cols, type_);
-        if (!empty()) std::memcpy(m.data, data, (size_t)rows * step);
+        for (int i = 0; i < rows && !empty(); ++i)
+            std::memcpy(m.data + (size_t)i * m.step, data + (size_t)i * step, m.step);
         return m;
     }
     template <typename T> T *ptr(int i) { return reinterpret_cast<T *>(data + (size_t)i * step); }
@@ -220,14 +221,23 @@ public:
             fail("process", "inputs must be CV_8UC1 of the constructed size (SGM.cpp:34-38)");
         this->img_l = img_l;  // shallow, as SGM.cpp:59-60 (decimated on the device)
         this->img_r = img_r;
-        const bool sky = !sky_mask.empty() && (bm_ || !sky_mask_beta.empty());
-        if (sky && (sky_mask.rows != img_h || sky_mask.cols != img_w ||
-                    (!bm_ && (sky_mask_beta.rows != img_h || sky_mask_beta.cols != img_w))))
-            fail("process", "sky masks must be CV_8UC1 on the working grid");
+        // Each mask applies on its own, as in the reference: sky_mask to the
+        // left DSI (Solver.cpp:146-178), sky_mask_beta to the right one
+        // (Solver.cpp:200-232); BM reads sky_mask only (BM.cpp:33-34).
+        const bool sky_l = !sky_mask.empty();
+        const bool sky_r = !bm_ && !sky_mask_beta.empty();
+        if (sky_l) check_mask(sky_mask, "sky_mask");
+        if (sky_r) check_mask(sky_mask_beta, "sky_mask_beta");
+        // The C-ABI takes one pitch for both masks: copy to a common (packed)
+        // pitch when the two masks' steps differ.
+        Mat ml = sky_mask, mr = sky_mask_beta;
+        if (sky_l && sky_r && ml.step != mr.step) {
+            ml = sky_mask.clone();
+            mr = sky_mask_beta.clone();
+        }
+        const int sky_pitch = sky_l ? (int)ml.step : sky_r ? (int)mr.step : 0;
         const int rc = sgm_process(handle_, img_l.data, img_r.data, (int)img_l.step,
-                                   sky ? sky_mask.data : nullptr,
-                                   sky && !bm_ ? sky_mask_beta.data : nullptr,
-                                   sky ? (int)sky_mask.step : 0,
+                                   sky_l ? ml.data : nullptr, sky_r ? mr.data : nullptr, sky_pitch,
                                    filtered_disp.template ptr<float>(0),
                                    (int)(filtered_disp.step / sizeof(float)), nullptr);
         if (rc != SGM_OK) fail("process", sgm_last_error(handle_));
@@ -250,6 +260,11 @@ protected:
 private:
     sgm_handle *handle_ = nullptr;
     bool bm_;
+
+    void check_mask(const Mat &m, const char *what) const {
+        if (m.type() != CV_8UC1 || m.rows != img_h || m.cols != img_w)
+            fail(what, "sky masks must be CV_8UC1 on the working grid (Solver.cpp:146,200)");
+    }
 
     static int device() {
         const char *e = std::getenv("SGM_AMD_DEVICE");

@@ -18,6 +18,17 @@
  * Threading: a handle is bound to one device and is not thread-safe (one
  * frame at a time, like the reference object, Solver.h:29-30).  Use one
  * handle per device/thread.
+ *
+ * Streams: every call on a handle uses the handle's device scratch (cost
+ * volumes, checkpoints, post-filter and LKRefine buffers), so the library
+ * orders calls made on different streams: a call whose stream differs from
+ * the previous call's first makes its stream wait for the previous call's
+ * work (an event recorded at the end of every call).  Calls on one stream
+ * are ordered by the stream itself.  Device entry points return after
+ * enqueueing, EXCEPT with post_filter: its median fill blocks the calling
+ * host thread on an event once per two fill launches to read a convergence
+ * counter (sgm_post_filter_device, and sgm_process_device with
+ * params.post_filter), so those calls are not fully asynchronous.
  */
 #ifndef SGM_HIP_H
 #define SGM_HIP_H

@@ -37,6 +37,8 @@ struct sgm_handle {
     hipStream_t st;       // the handle's own stream (host API, stages)
     hipStream_t aux[1];      // right view (two-view frames)
     hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1, ev_pf;
+    hipEvent_t ev_last;   // end of the last entry point's work (StreamScope)
+    hipStream_t last_st;  // ... and the stream it ran on (null: none yet)
     uint8_t *d_in[2];     // full-size input staging (host API)
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
@@ -84,6 +86,24 @@ struct DeviceGuard {
     ~DeviceGuard() {
         int cur = -1;
         if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Every entry point's work shares the handle's scratch (cost volumes,
+// checkpoints, post-filter and LKRefine buffers), whichever stream the caller
+// passes.  A StreamScope orders calls on different streams: if this call's
+// stream differs from the previous call's, it first waits for the event the
+// previous call recorded at its end; on leaving it records that event on its
+// own stream.  Calls on one stream pay only the record.
+struct StreamScope {
+    sgm_handle *h;
+    hipStream_t st;
+    StreamScope(sgm_handle *handle, void *stream)
+        : h(handle), st(stream ? (hipStream_t)stream : handle->st) {
+        if (h->last_st && h->last_st != st) (void)hipStreamWaitEvent(st, h->ev_last, 0);
+    }
+    ~StreamScope() {
+        if (hipEventRecord(h->ev_last, st) == hipSuccess) h->last_st = st;
     }
 };
 
@@ -179,7 +199,7 @@ void free_all(sgm_handle *h) {
     if (h->st) (void)hipStreamDestroy(h->st);
     for (auto &s : h->aux) if (s) (void)hipStreamDestroy(s);
     hipEvent_t evs[] = {h->ev_ct, h->ev_c[0], h->ev_c[1], h->ev_t[0], h->ev_t[1],
-                        h->ev_s[0], h->ev_s[1], h->ev_v1, h->ev_pf};
+                        h->ev_s[0], h->ev_s[1], h->ev_v1, h->ev_pf, h->ev_last};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -633,7 +653,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
         if (rc) break;
         hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1],
-                             &h->ev_s[0], &h->ev_s[1], &h->ev_v1, &h->ev_pf};
+                             &h->ev_s[0], &h->ev_s[1], &h->ev_v1, &h->ev_pf,
+                             &h->ev_last};
         for (auto e : evs)
             if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { rc = SGM_ERR_HIP; break; }
         if (rc) break;
@@ -723,7 +744,8 @@ int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_ri
     if (h->p.aux_only)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process_device: handle created with aux_only");
     DeviceGuard guard(h->device);
-    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    StreamScope scope(h, stream);
+    hipStream_t st = scope.st;
     return run_frame(h, d_left, d_right, pitch, d_sky_l, d_sky_r, sky_pitch, d_out, out_pitch,
                      d_raw_disp, st);
 }
@@ -738,6 +760,7 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
     if (h->p.aux_only)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: handle created with aux_only");
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     int rc;
     if ((rc = ensure_pinned(h))) return rc;
     const size_t nin = (size_t)h->p.height * h->p.width, npx = (size_t)h->g.H * h->g.W;
@@ -860,6 +883,7 @@ int sgm_post_filter_host(float *F, int H, int W, int D, int scale) {
 int sgm_stage_census(sgm_handle *h, const uint8_t *img, int pitch, uint64_t *ct) {
     if (!h || !img || !ct || pitch < h->p.width) return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     int rc;
     if ((rc = copy_in_image(h, h->d_in[0], img, pitch))) return rc;
     HIPCHK(h, sgm::launch_census(h->d_in[0], h->p.width, h->g, h->p.blur, h->d_ct[0], h->st));
@@ -874,6 +898,7 @@ int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr, cons
     if (!h || !ctl || !ctr || !cost || (view != 0 && view != 1)) return SGM_ERR_INVALID_ARG;
     if (h->p.aux_only) return set_err(h, SGM_ERR_INVALID_ARG, "stage needs cost volumes (aux_only)");
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_ct[0], ctl, npx * 8, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, hipMemcpyAsync(h->d_ct[1], ctr, npx * 8, hipMemcpyHostToDevice, h->st));
@@ -896,6 +921,7 @@ int sgm_stage_path(sgm_handle *h, int dir, const float *cost, float *L, float *m
     if (!h || !cost || !L || dir < 0 || dir > 7) return SGM_ERR_INVALID_ARG;
     if (h->p.aux_only) return set_err(h, SGM_ERR_INVALID_ARG, "stage needs cost volumes (aux_only)");
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
     SweepArgs a = sweep_args(h);
@@ -913,6 +939,7 @@ int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float 
     if (!h || !cost) return SGM_ERR_INVALID_ARG;
     if (h->p.aux_only) return set_err(h, SGM_ERR_INVALID_ARG, "stage needs cost volumes (aux_only)");
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, hipEventRecord(h->ev_c[0], h->st));
@@ -934,7 +961,8 @@ int sgm_lr_check_device(sgm_handle *h, const float *d_fl, int fl_pitch, const fl
     if (d_out == d_fr)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_lr_check_device: d_out must not alias d_fr");
     DeviceGuard guard(h->device);
-    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    StreamScope scope(h, stream);
+    hipStream_t st = scope.st;
     HIPCHK(h, timed(h, "lr", (double)h->g.H * W, st, [&] {
                return sgm::launch_lr(d_fl, fl_pitch, d_fr, fr_pitch, d_out, out_pitch,
                                      h->p.lr_max_diff, h->g, st);
@@ -947,7 +975,8 @@ int sgm_post_filter_device(sgm_handle *h, float *d_disp, int pitch, void *stream
     if (!d_disp || pitch < h->g.W)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_post_filter_device: bad pointer or pitch");
     DeviceGuard guard(h->device);
-    return post_filter(h, d_disp, pitch, stream ? (hipStream_t)stream : h->st);
+    StreamScope scope(h, stream);
+    return post_filter(h, d_disp, pitch, scope.st);
 }
 
 int sgm_lk_refine_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
@@ -956,14 +985,15 @@ int sgm_lk_refine_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_
     if (!d_left || !d_right || !d_disp || pitch < h->p.width || disp_pitch < h->g.W)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_lk_refine_device: bad pointer or pitch");
     DeviceGuard guard(h->device);
-    return lk_refine(h, d_left, d_right, pitch, d_disp, disp_pitch,
-                     stream ? (hipStream_t)stream : h->st);
+    StreamScope scope(h, stream);
+    return lk_refine(h, d_left, d_right, pitch, d_disp, disp_pitch, scope.st);
 }
 
 int sgm_stage_lk_refine(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pitch,
                         float *disp) {
     if (!h || !left || !right || !disp || pitch < h->p.width) return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W;
     int rc;
     if ((rc = copy_in_image(h, h->d_in[0], left, pitch))) return rc;
@@ -981,7 +1011,8 @@ int sgm_sky_detect_device(sgm_handle *h, const uint8_t *d_img, int pitch, uint8_
     if (!d_img || !d_mask || pitch < h->p.width || mask_pitch < h->g.W)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_sky_detect_device: bad pointer or pitch");
     DeviceGuard guard(h->device);
-    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    StreamScope scope(h, stream);
+    hipStream_t st = scope.st;
     HIPCHK(h, timed(h, "sky_detect", (double)h->g.H * h->g.W, st, [&] {
                return sgm::launch_sky_detect(&d_img, pitch, &d_mask, mask_pitch, h->d_sky_scratch,
                                              1, h->g, st);
@@ -992,6 +1023,7 @@ int sgm_sky_detect_device(sgm_handle *h, const uint8_t *d_img, int pitch, uint8_
 int sgm_stage_sky_detect(sgm_handle *h, const uint8_t *img, int pitch, uint8_t *mask) {
     if (!h || !img || !mask || pitch < h->p.width) return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W;
     int rc;
     if ((rc = copy_in_image(h, h->d_in[0], img, pitch))) return rc;
@@ -1008,7 +1040,8 @@ int sgm_colormap_device(sgm_handle *h, const float *d_disp, int pitch, uint8_t *
     if (!d_disp || !d_bgr || pitch < h->g.W || bgr_pitch < 3 * h->g.W)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_colormap_device: bad pointer or pitch");
     DeviceGuard guard(h->device);
-    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    StreamScope scope(h, stream);
+    hipStream_t st = scope.st;
     HIPCHK(h, timed(h, "colormap", (double)h->g.H * h->g.W, st, [&] {
                return sgm::launch_colormap(d_disp, pitch, d_bgr, bgr_pitch, h->g, st);
            }));
@@ -1023,7 +1056,8 @@ int sgm_point_cloud_device(sgm_handle *h, const float *d_disp, int pitch, const 
         img_pitch < h->g.W)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_point_cloud_device: bad pointer or pitch");
     DeviceGuard guard(h->device);
-    hipStream_t st = stream ? (hipStream_t)stream : h->st;
+    StreamScope scope(h, stream);
+    hipStream_t st = scope.st;
     HIPCHK(h, timed(h, "point_cloud", (double)h->g.H * h->g.W, st, [&] {
                return sgm::launch_point_cloud(d_disp, pitch, d_img, img_pitch, cam->fx, cam->fy,
                                               cam->cx, cam->cy, cam->baseline, cam->max_range,
@@ -1036,6 +1070,7 @@ int sgm_point_cloud_device(sgm_handle *h, const float *d_disp, int pitch, const 
 int sgm_stage_colormap(sgm_handle *h, const float *disp, uint8_t *bgr) {
     if (!h || !disp || !bgr) return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W;
     // staging: the map in d_out, the BGR image over the two working-grid sky masks' space
     uint8_t *d_bgr = nullptr;
@@ -1055,6 +1090,7 @@ int sgm_stage_point_cloud(sgm_handle *h, const float *disp, const uint8_t *img, 
     if (!h || !disp || !img || !cam || !xyz || !pixel || !count || img_pitch < h->g.W)
         return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W;
     const int rows_used = h->g.H;  // the node reads img(i, j) at working-grid indices
     uint8_t *d_img = nullptr, *d_pix = nullptr;
@@ -1087,6 +1123,7 @@ int sgm_stage_point_cloud(sgm_handle *h, const float *disp, const uint8_t *img, 
 int sgm_stage_post_filter(sgm_handle *h, float *disp) {
     if (!h || !disp) return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W;
     HIPCHK(h, hipMemcpyAsync(h->d_out, disp, npx * 4, hipMemcpyHostToDevice, h->st));
     int rc = post_filter(h, h->d_out, h->g.W, h->st);
@@ -1099,6 +1136,7 @@ int sgm_stage_post_filter(sgm_handle *h, float *disp) {
 int sgm_stage_lr(sgm_handle *h, const float *fl, const float *fr, float *out) {
     if (!h || !fl || !fr || !out) return SGM_ERR_INVALID_ARG;
     DeviceGuard guard(h->device);
+    StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W;
     HIPCHK(h, hipMemcpyAsync(h->d_sub[0], fl, npx * 4, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, hipMemcpyAsync(h->d_sub[1], fr, npx * 4, hipMemcpyHostToDevice, h->st));

@@ -26,11 +26,17 @@ def gather_maps(local: torch.Tensor, n_items: int, group=None) -> torch.Tensor |
     """Gathers every rank's stack of maps (k_r x H x W, k_r = len(shard(...)))
     to rank 0 and returns the n_items x H x W batch in item order there (None
     on other ranks).  Ranks holding fewer items pad with a zero map so one
-    fixed-size gather serves uneven batches."""
+    fixed-size gather serves uneven batches.  Every rank's `local` must carry
+    the same H x W, dtype and device type (a rank with no items passes an
+    empty 0 x H x W stack of them); n_items == 0 gathers nothing."""
+    if local.dim() != 3:
+        raise ValueError(f"local must be a k x H x W stack, got shape {tuple(local.shape)}")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    per = (n_items + world - 1) // world
     h, w = local.shape[-2:]
+    if n_items == 0:
+        return torch.empty((0, h, w), dtype=local.dtype, device=local.device) if rank == 0 else None
+    per = (n_items + world - 1) // world
     send = torch.zeros((per, h, w), dtype=local.dtype, device=local.device)
     if local.shape[0]:
         send[: local.shape[0]] = local
@@ -45,17 +51,27 @@ def gather_maps(local: torch.Tensor, n_items: int, group=None) -> torch.Tensor |
     return out
 
 
-def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], group=None):
+def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], map_shape,
+                  *, dtype=torch.float32, device="cpu", group=None):
     """Runs `compute(pair) -> H x W map` on this rank's shard of `pairs` and
-    gathers the maps to rank 0 (returned there, None elsewhere)."""
+    gathers the maps to rank 0 (returned there, None elsewhere).
+
+    `map_shape` (H, W), `dtype` and `device` describe the maps `compute`
+    returns (for an SGM handle: (rows, cols), float32, its cuda device): a
+    rank whose shard is empty (fewer pairs than ranks) sends a zero stack of
+    that kind without computing a frame, so the gather's buffers agree on
+    every rank (RCCL needs them on the GPU, gloo on the host)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    h, w = map_shape
     mine = [compute(pairs[i]) for i in shard(len(pairs), rank, world)]
+    for m in mine:
+        if tuple(m.shape) != (h, w):
+            raise ValueError(f"compute returned a {tuple(m.shape)} map, expected {(h, w)}")
     if mine:
-        local = torch.stack(mine)
+        local = torch.stack([m.to(device=device, dtype=dtype) for m in mine])
     else:
-        h, w = compute(pairs[0]).shape  # shape only; no rank holds zero pairs when n >= world
-        local = torch.empty((0, h, w))
+        local = torch.empty((0, h, w), dtype=dtype, device=device)
     return gather_maps(local, len(pairs), group)
 
 

@@ -102,12 +102,21 @@ class SGM:
             _u8(sky_mask, (self.rows, self.cols), "sky_mask")
         sr = None if sky_mask_beta is None or np.size(sky_mask_beta) == 0 else \
             _u8(sky_mask_beta, (self.rows, self.cols), "sky_mask_beta")
+        # Fresh output maps per frame: the arrays handed out by get_disp() /
+        # get_lr_disp() / get_raw_disp() for one frame are never overwritten
+        # by the next (the reference's get_disp() reference is valid until the
+        # next process(), inc/Solver.h:36; a copy-free handle-owned buffer
+        # would alias the previous frame's result).
+        out = np.empty((self.rows, self.cols), np.float32)
+        raw = np.empty((self.rows, self.cols), np.uint16)
         check(self._lib.sgm_process(self._h, _ptr(l), _ptr(r), self.w, _ptr(sl), _ptr(sr),
-                                    self.cols, _ptr(self._lr), self.cols, _ptr(self._raw)),
+                                    self.cols, _ptr(out), self.cols, _ptr(raw)),
               self._h)
-        self._final = None
+        self._raw = raw
         if self.params.post_filter or self.params.lk_refine:  # sgm_process returned the final map
-            self._final, self._lr = self._lr, None
+            self._final, self._lr = out, None
+        else:
+            self._final, self._lr = None, out
 
     def process_device(self, d_left: int, d_right: int, d_out: int, *, pitch: int | None = None,
                        d_sky_l: int = 0, d_sky_r: int = 0, sky_pitch: int | None = None,

@@ -64,6 +64,36 @@ int main(int argc, char **argv) {
             fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
         return fo ? 0 : 4;
     }
+    if (argc == 10 && std::string(argv[1]) == "runsky") {
+        // process(l, r, sky, sky_beta) with either mask possibly "-" (empty);
+        // the beta mask is held with a wider row pitch than the left one
+        const int h = std::atoi(argv[6]), w = std::atoi(argv[7]), d = std::atoi(argv[8]);
+        Mat l(h, w, CV_8UC1), r(h, w, CV_8UC1), sl, sr;
+        std::ifstream fl(argv[2], std::ios::binary), fr(argv[3], std::ios::binary);
+        fl.read(reinterpret_cast<char *>(l.data), (std::streamsize)h * w);
+        fr.read(reinterpret_cast<char *>(r.data), (std::streamsize)h * w);
+        if (!fl || !fr) return 2;
+        if (std::string(argv[4]) != "-") {
+            sl.create(h, w, CV_8UC1);
+            std::ifstream f(argv[4], std::ios::binary);
+            f.read(reinterpret_cast<char *>(sl.data), (std::streamsize)h * w);
+            if (!f) return 2;
+        }
+        if (std::string(argv[5]) != "-") {
+            sr.create(h, w + 24, CV_8UC1);
+            sr.cols = w;  // a pitched view: step = w + 24 bytes
+            std::ifstream f(argv[5], std::ios::binary);
+            for (int i = 0; i < h; ++i) f.read(reinterpret_cast<char *>(sr.ptr<unsigned char>(i)), w);
+            if (!f) return 2;
+        }
+        sgm_amd::SGM sgm(h, w, 1, d);
+        sgm.process(l, r, sl, sr);
+        const Mat &disp = sgm.get_disp();
+        std::ofstream fo(argv[9], std::ios::binary);
+        for (int i = 0; i < disp.rows; ++i)
+            fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
+        return fo ? 0 : 4;
+    }
     if (argc == 7 && std::string(argv[1]) == "sky") {
         const int h = std::atoi(argv[3]), w = std::atoi(argv[4]), s = std::atoi(argv[5]);
         Mat img(h, w, CV_8UC1), mask;

@@ -112,3 +112,36 @@ def test_lk_wrapper_matches_oracle(exe, tmp_path):
     got = np.fromfile(paths[3], np.float32).reshape(h, w)
     want = oracle.lk_refine(left, right, disp, D)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("masks", ["left", "right", "both"])
+def test_class_surface_one_sided_sky_masks(exe, tmp_path, masks):
+    # process(l, r, sky, sky_beta): each mask applies to its own view
+    # (Solver.cpp:146-178 left DSI, :200-232 right DSI), also when the other
+    # one is empty; the beta mask comes with a different row pitch
+    import oracle
+    oracle.build()
+    h, w, D = 72, 220, 64
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=8)
+    sky = synthetic.sky_mask(h, w)
+    sl = sky if masks in ("left", "both") else None
+    sr = sky if masks in ("right", "both") else None
+    paths = {n: str(tmp_path / n) for n in ("l", "r", "sl", "sr", "out")}
+    left.tofile(paths["l"])
+    right.tofile(paths["r"])
+    args = [exe, "runsky", paths["l"], paths["r"], "-", "-", str(h), str(w), str(D), paths["out"]]
+    if sl is not None:
+        sl.tofile(paths["sl"])
+        args[4] = paths["sl"]
+    if sr is not None:
+        sr.tofile(paths["sr"])
+        args[5] = paths["sr"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(paths["out"], dtype=np.float32).reshape(h, w)
+    want = oracle.process(left, right, D, sky_l=sl, sky_r=sr)["final"]
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    if masks != "both":   # a one-sided mask is not silently dropped
+        none = oracle.process(left, right, D)["final"]
+        assert not np.array_equal(got.view(np.uint32), none.view(np.uint32))

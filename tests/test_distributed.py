@@ -18,8 +18,8 @@ from stereo_matching_amd import distributed, synthetic
 H, W, D, N = 24, 80, 32, 5
 
 
-def _pairs():
-    return [synthetic.stereo_pair(H, W, D, pair_index=i) for i in range(N)]
+def _pairs(n=N):
+    return [synthetic.stereo_pair(H, W, D, pair_index=i) for i in range(n)]
 
 
 def _compute(pair):
@@ -27,11 +27,21 @@ def _compute(pair):
     return torch.from_numpy(oracle.process(pair[0], pair[1], D, views=1)["sub"])
 
 
-def _worker(rank, world, port, q):
+_CALLS = []
+
+
+def _counting_compute(pair):
+    _CALLS.append(1)
+    return _compute(pair)
+
+
+def _worker(rank, world, port, q, n=N):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = distributed.process_batch(_pairs(), _compute)
+        out = distributed.process_batch(_pairs(n), _counting_compute, (H, W))
+        # a rank computes exactly its shard: no extra frame to learn the shape
+        assert len(_CALLS) == len(distributed.shard(n, rank, world)), (rank, len(_CALLS))
         q.put((rank, None if out is None else out.numpy()))
     finally:
         dist.destroy_process_group()
@@ -52,13 +62,16 @@ def test_shard_round_robin():
         distributed.shard(4, 2, 2)
 
 
-def test_gather_world2_gloo():
+@pytest.mark.parametrize("n", [N, 1, 0])
+def test_gather_world2_gloo(n):
+    # n = 1: rank 1 holds no pair and sends an empty stack of the right kind;
+    # n = 0: nothing to gather, rank 0 gets a 0 x H x W batch
     import oracle
     oracle.build()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, n)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -66,9 +79,10 @@ def test_gather_world2_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[1] is None
-    want = np.stack([_compute(p).numpy() for p in _pairs()])
-    assert res[0].shape == (N, H, W)
-    assert np.array_equal(res[0].view(np.uint32), want.view(np.uint32))
+    assert res[0].shape == (n, H, W) and res[0].dtype == np.float32
+    if n:
+        want = np.stack([_compute(p).numpy() for p in _pairs(n)])
+        assert np.array_equal(res[0].view(np.uint32), want.view(np.uint32))
 
 
 def _pipe_worker(rank, world, port, q):

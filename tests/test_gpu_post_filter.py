@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 import postfilter_maps
-from stereo_matching_amd import SGM, synthetic
+from stereo_matching_amd import BM, SGM, synthetic
 
 pytestmark = pytest.mark.gpu
 
@@ -107,7 +107,7 @@ sys.path.insert(0, sys.argv[1])
 dev = torch.device("cuda", 0)
 torch.cuda.init()                      # torch's runtime first, as in bench.py
 import oracle
-from stereo_matching_amd import SGM, synthetic
+from stereo_matching_amd import BM, SGM, synthetic
 h, w, D = 96, 260, 64
 left, right = synthetic.stereo_pair(h, w, D, pair_index=2, kind="noise")
 ref = oracle.process(left, right, D)
@@ -144,3 +144,30 @@ def test_post_filter_repeatable():
         first = check_map(sgm, F, D, 1)
         for _ in range(3):
             assert np.array_equal(bits(sgm.post_filter(F)), bits(first))
+
+
+@pytest.mark.parametrize("kind", ["post_filter", "lk_refine", "bm"])
+def test_process_twice_on_one_handle(kind):
+    # every process() on a post_filter / lk_refine / BM handle writes a fresh
+    # final map (the second call used to pass a NULL output), and
+    # the map handed out for frame 1 is not overwritten by frame 2
+    h, w, D = 64, 200, 64
+    pairs = [synthetic.stereo_pair(h, w, D, pair_index=k, kind=("noise" if k else "road"))
+             for k in range(3)]
+    if kind == "bm":
+        want = [oracle.post_filter(oracle.bm_process(l, r, D, 1).astype(np.float32), D, 1)
+                for l, r in pairs]
+        handle = BM(h, w, 1, D, device=0)
+    elif kind == "lk_refine":
+        want = [oracle.lk_refine(l, r, oracle.process(l, r, D)["final"], D) for l, r in pairs]
+        handle = SGM(h, w, 1, D, device=0, post_filter=True, lk_refine=True)
+    else:
+        want = [oracle.process(l, r, D)["final"] for l, r in pairs]
+        handle = SGM(h, w, 1, D, device=0, post_filter=True)
+    with handle as sgm:
+        kept = []
+        for l, r in pairs:
+            sgm.process(l, r)
+            kept.append(sgm.get_disp())
+        for k in range(len(pairs)):
+            assert np.array_equal(bits(kept[k]), bits(want[k])), k

@@ -61,3 +61,46 @@ def test_joint_final_matches_per_view():
     h, w, D = 512, 1056, 128
     assert h * w * D * 4 > 256 * 1024 * 1024
     _same(_run(h, w, D, False, False, {}), _run(h, w, D, False, False, {"SGM_SPLIT_FINAL": "1"}))
+
+
+CROSS_STREAM = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+dev = torch.device("cuda", 0)
+torch.cuda.init()
+import oracle
+from stereo_matching_amd import SGM, synthetic
+h, w, D = 200, 640, 128
+pairs = [synthetic.stereo_pair(h, w, D, pair_index=k, kind=("road", "noise")[k % 2]) for k in range(4)]
+want = [oracle.process(l, r, D)["final"] for l, r in pairs]
+streams = [torch.cuda.Stream(dev) for _ in range(3)]
+imgs = [(torch.from_numpy(l).to(dev), torch.from_numpy(r).to(dev)) for l, r in pairs]
+outs = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in pairs]
+torch.cuda.synchronize(dev)
+with SGM(h, w, 1, D, device=0) as sgm:
+    # frame k on stream k % 3, its post filter on stream (k + 1) % 3, with no
+    # host synchronisation in between: the handle orders the calls (they
+    # share its cost volumes and post-filter scratch)
+    for k, ((l, r), out) in enumerate(zip(imgs, outs)):
+        sa, sb = streams[k % 3], streams[(k + 1) % 3]
+        for t in (l, r, out):
+            t.record_stream(sa)
+        out.record_stream(sb)
+        sgm.process_device(l.data_ptr(), r.data_ptr(), out.data_ptr(), stream=sa.cuda_stream)
+        sgm.post_filter_device(out.data_ptr(), stream=sb.cuda_stream)
+    torch.cuda.synchronize(dev)
+for k, out in enumerate(outs):
+    got = out.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), want[k].view(np.uint32)), k
+print("cross-stream ok")
+"""
+
+
+def test_calls_on_different_streams_are_ordered():
+    # ADVICE r01: per-handle scratch shared by calls on different streams
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", CROSS_STREAM, root], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "cross-stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
