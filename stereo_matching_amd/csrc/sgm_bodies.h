@@ -760,7 +760,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                     *reinterpret_cast<float4 *>(row + k) = x4;
                 }
             }
-            wta_consume_chunk_at<V, KP>(F->t[c & 1] + half * KP,
+            wta_chunk_q<V, KP, QQ>(F->t[c & 1] + half * KP,
                                         (long long)(H - 1 - c * K - half * KP) * W + path,
                                         -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
             bar();

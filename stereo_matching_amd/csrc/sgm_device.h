@@ -546,6 +546,94 @@ __device__ __forceinline__ void wta_consume_chunk_at(const float (*tb)[tbuf_stri
     }
 }
 
+// Minimum over an LPP-lane group (LPP = 4..32 consecutive lanes), in every
+// lane of the group: quad, half-row and row mirrors, then the 16-apart
+// swizzle for 32-lane groups.
+template <int LPP>
+__device__ __forceinline__ float group_min(float x) {
+    x = fminf(x, movdppf<DPP_QP_1032>(x));
+    x = fminf(x, movdppf<DPP_QP_2301>(x));
+    if constexpr (LPP >= 8) x = fminf(x, movdppf<DPP_HALF_MIRROR>(x));
+    if constexpr (LPP >= 16) x = fminf(x, movdppf<DPP_MIRROR>(x));
+    if constexpr (LPP >= 32)
+        x = fminf(x, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x1F | (0x10 << 10))));
+    return x;
+}
+template <int LPP>
+__device__ __forceinline__ int group_min_i(int x) {
+    x = min(x, movdpp<DPP_QP_1032>(x));
+    x = min(x, movdpp<DPP_QP_2301>(x));
+    if constexpr (LPP >= 8) x = min(x, movdpp<DPP_HALF_MIRROR>(x));
+    if constexpr (LPP >= 16) x = min(x, movdpp<DPP_MIRROR>(x));
+    if constexpr (LPP >= 32) x = min(x, __builtin_amdgcn_ds_swizzle(x, 0x1F | (0x10 << 10)));
+    return x;
+}
+
+// The same WTA + uniqueness + sub-pixel for `cnt` <= PF pixels of a chunk,
+// with the disparities per lane (QQ) known at compile time: instead of a
+// running (min, index, second, index) state merged across lanes (about 15
+// VALU ops per disparity and per merge step), two group minima of the values
+// and two of the first indices holding them:
+//   m  = min_d S[d],                     min_d = min { d : S[d] == m }
+//   s  = min { S[d] : S[d] != m },       sec_d = min { d : S[d] == s }
+// (SGM.cpp:383-408: the first strict minimum, the smallest other value and
+// its first index).
+template <int V, int PF, int QQ>
+__device__ __forceinline__ void wta_chunk_q(const float (*tb)[tbuf_stride<V>()], long long pix0,
+                                            long long pix_step, int cnt, int lane, int Dn,
+                                            float uniq, uint16_t *disp, float *sub) {
+    constexpr int LPP = 64 / PF;  // lanes per pixel
+    static_assert(QQ % 4 == 0 && LPP <= 32, "float4 rows, at most 32 lanes per pixel");
+    const int px = lane / LPP, q = lane - px * LPP;
+    const int d0 = q * QQ;
+    const float *row = tb[px < cnt ? px : 0];
+    float x[QQ];
+#pragma unroll
+    for (int k = 0; k < QQ; k += 4) {
+        const float4 x4 = *reinterpret_cast<const float4 *>(row + d0 + k);
+        x[k] = x4.x; x[k + 1] = x4.y; x[k + 2] = x4.z; x[k + 3] = x4.w;
+    }
+    float lm = x[0];
+#pragma unroll
+    for (int k = 1; k < QQ; ++k) lm = fminf(lm, x[k]);
+    const float m = group_min<LPP>(lm);
+    // first index of m in this lane (QQ: none), and the lane's smallest value != m
+    int li = QQ;
+    float ls = SGM_INF;
+#pragma unroll
+    for (int k = QQ - 1; k >= 0; --k) {
+        const bool eq = x[k] == m;
+        li = eq ? k : li;
+        ls = eq ? ls : fminf(ls, x[k]);
+    }
+    const int mi = group_min_i<LPP>(li < QQ ? d0 + li : INT_MAX);
+    const float sec = group_min<LPP>(ls);
+    int d = mi;
+    if (sec != SGM_INF) {  // a second distinct value exists (else sec = FLT_MAX: ratio ~ 0)
+        int lj = QQ;
+#pragma unroll
+        for (int k = QQ - 1; k >= 0; --k) lj = x[k] == sec ? k : lj;
+        const int si = group_min_i<LPP>(lj < QQ ? d0 + lj : INT_MAX);
+        if (m / sec > uniq && abs(mi - si) > 1) d = Dn + 1;
+    }
+    float f;
+    if (d > Dn - 1) {
+        f = (float)(Dn + 1);
+    } else if (d == 0 || d == Dn - 1) {
+        f = (float)d;
+    } else {
+        const float av = row[d - 1], bv = row[d + 1], cv = row[d];
+        const float xx = d + (av - bv) / (2 * (av + bv - 2 * cv));
+        const float lim = (Dn - 1) * 1.f;
+        f = (lim < xx) ? lim : xx;  // std::min(x, lim)
+    }
+    if (q == 0 && px < cnt) {
+        const long long pix = pix0 + px * pix_step;
+        disp[pix] = (uint16_t)d;
+        sub[pix] = f;
+    }
+}
+
 template <int V, int PF>
 __device__ __forceinline__ void wta_consume_chunk(const float (*tb)[tbuf_stride<V>()],
                                                   const long long *pb, int cnt, int lane,
