@@ -748,21 +748,23 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             tload(tn, c + 2 < nseg ? c + 2 : nseg - 1);
             const int cnt_all = c == nseg - 1 ? r0 : K;
             const int cnt = cnt_all - half * KP < 0 ? 0 : (cnt_all - half * KP > KP ? KP : cnt_all - half * KP);
-            if (px < cnt) {
-                float *row = &F->t[c & 1][slot][d0];
+            // total = X + T in registers (the WTA's own lane layout); the row
+            // goes back to LDS only for the sub-pixel's three neighbours
+            float *row = &F->t[c & 1][slot][d0];
+            float x[QQ];
 #pragma unroll
-                for (int k = 0; k < QQ; k += 4) {
-                    float4 x4 = *reinterpret_cast<float4 *>(row + k);
-                    x4.x = x4.x + t[k];
-                    x4.y = x4.y + t[k + 1];
-                    x4.z = x4.z + t[k + 2];
-                    x4.w = x4.w + t[k + 3];
-                    *reinterpret_cast<float4 *>(row + k) = x4;
-                }
+            for (int k = 0; k < QQ; k += 4) {
+                float4 x4 = *reinterpret_cast<float4 *>(row + k);
+                x4.x = x4.x + t[k];
+                x4.y = x4.y + t[k + 1];
+                x4.z = x4.z + t[k + 2];
+                x4.w = x4.w + t[k + 3];
+                x[k] = x4.x; x[k + 1] = x4.y; x[k + 2] = x4.z; x[k + 3] = x4.w;
+                if (px < cnt) *reinterpret_cast<float4 *>(row + k) = x4;
             }
-            wta_chunk_q<V, KP, QQ>(F->t[c & 1] + half * KP,
-                                        (long long)(H - 1 - c * K - half * KP) * W + path,
-                                        -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
+            wta_chunk_q<V, KP, QQ>(x, F->t[c & 1] + half * KP,
+                                   (long long)(H - 1 - c * K - half * KP) * W + path,
+                                   -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
             bar();
         };
         float t0[QQ], t1[QQ], t2[QQ];

@@ -578,21 +578,17 @@ __device__ __forceinline__ int group_min_i(int x) {
 //   s  = min { S[d] : S[d] != m },       sec_d = min { d : S[d] == s }
 // (SGM.cpp:383-408: the first strict minimum, the smallest other value and
 // its first index).
+// x: this lane's QQ total costs (disparities d0 .. d0+QQ-1 of pixel px); the
+// LDS rows tb[] hold the same totals for the sub-pixel's neighbours.
 template <int V, int PF, int QQ>
-__device__ __forceinline__ void wta_chunk_q(const float (*tb)[tbuf_stride<V>()], long long pix0,
-                                            long long pix_step, int cnt, int lane, int Dn,
-                                            float uniq, uint16_t *disp, float *sub) {
+__device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*tb)[tbuf_stride<V>()],
+                                            long long pix0, long long pix_step, int cnt, int lane,
+                                            int Dn, float uniq, uint16_t *disp, float *sub) {
     constexpr int LPP = 64 / PF;  // lanes per pixel
-    static_assert(QQ % 4 == 0 && LPP <= 32, "float4 rows, at most 32 lanes per pixel");
+    static_assert(QQ % 4 == 0 && LPP <= 32, "QQ a multiple of 4, at most 32 lanes per pixel");
     const int px = lane / LPP, q = lane - px * LPP;
     const int d0 = q * QQ;
     const float *row = tb[px < cnt ? px : 0];
-    float x[QQ];
-#pragma unroll
-    for (int k = 0; k < QQ; k += 4) {
-        const float4 x4 = *reinterpret_cast<const float4 *>(row + d0 + k);
-        x[k] = x4.x; x[k + 1] = x4.y; x[k + 2] = x4.z; x[k + 3] = x4.w;
-    }
     float lm = x[0];
 #pragma unroll
     for (int k = 1; k < QQ; ++k) lm = fminf(lm, x[k]);
