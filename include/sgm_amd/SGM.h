@@ -247,12 +247,14 @@ public:
     sgm_handle *handle() const { return handle_; }
 
 protected:
-    HipSolver(int h, int w, int s, int d, int solver) : Solver(h, w, s, d), bm_(solver == SGM_SOLVER_BM) {
+    // views = 1: the left view alone (BM; GPU_SGM, gpu_sgm/src/SGM.cu:105-232)
+    HipSolver(int h, int w, int s, int d, int solver, int views = 2)
+        : Solver(h, w, s, d), bm_(solver == SGM_SOLVER_BM) {
         sgm_params p;
         if (sgm_default_params(&p, h, w, s, d) != SGM_OK) fail("Solver", "sgm_default_params");
         p.solver = solver;
         p.post_filter = 1;  // process() ends with post_filter(): SGM.cpp:821, BM.cpp:88 (on the GPU)
-        if (bm_) p.views = 1;
+        p.views = bm_ ? 1 : views;
         const int rc = sgm_create(&p, device(), &handle_);
         if (rc != SGM_OK) fail("sgm_create", handle_ ? sgm_last_error(handle_) : "no device");
     }

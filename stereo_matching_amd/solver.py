@@ -294,3 +294,16 @@ class BM(SGM):
                  blur: bool = True, uniqueness: float = 0.7, sky_detect: bool = False):
         super().__init__(h, w, s, d, device=device, blur=blur, views=1, uniqueness=uniqueness,
                          post_filter=True, sky_detect=sky_detect, _solver=_capi.SGM_SOLVER_BM)
+
+
+class GPU_SGM(SGM):
+    """Mirrors the reference's CUDA backend class ``GPU_SGM(int h, int w, int s,
+    int d)`` (gpu_sgm/inc/SGM.cuh:23-62; node.cpp:50 holds its commented-out
+    call site): process(l, r) runs the LEFT view only -- SGM, WTA, sub-pixel,
+    then post_filter (gpu_sgm/src/SGM.cu:105-232) -- and get_disp() returns
+    that post-filtered map.  Results follow the reference's CPU path bit for bit
+    (src/SGM.cpp:32-443, Solver.cpp:569-649), not the CUDA tree's
+    approximations."""
+
+    def __init__(self, h: int, w: int, s: int = 1, d: int = 128, *, device: int = 0):
+        super().__init__(h, w, s, d, device=device, views=1, post_filter=True)

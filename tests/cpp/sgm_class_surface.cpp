@@ -4,10 +4,14 @@
 //   sgm_class_surface nodevice            -> argument asserts + no-device error
 //   sgm_class_surface run L R H W D OUT   -> raw u8 pair in, f32 disparity out
 //   sgm_class_surface runbm L R H W D OUT -> the same through BM(h, w, s, d)
+//   sgm_class_surface rungpu L R H W S D OUT OUT2 -> GPU_SGM(h, w, s, d) as node.cpp:50
+//                                         would build it: get_disp() to OUT, and to
+//                                         OUT2 again after show_disp()
 //   sgm_class_surface sky IMG H W S OUT   -> SkyAreaDetector::detect mask
 //   sgm_class_surface lk L R DISP H W D OUT -> LKSubPixel::LKRefine of DISP
 #define SGM_AMD_THROW 1
 #include "sgm_amd/SGM.h"
+#include "sgm_amd/GPU_SGM.h"
 #include "sgm_amd/LKSubPixel.h"
 #include "sgm_amd/SkyAreaDetector.h"
 
@@ -63,6 +67,29 @@ int main(int argc, char **argv) {
         for (int i = 0; i < disp.rows; ++i)
             fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
         return fo ? 0 : 4;
+    }
+    if (argc == 10 && std::string(argv[1]) == "rungpu") {
+        const int h = std::atoi(argv[4]), w = std::atoi(argv[5]), s = std::atoi(argv[6]),
+                  d = std::atoi(argv[7]);
+        Mat l(h, w, CV_8UC1), r(h, w, CV_8UC1);
+        std::ifstream fl(argv[2], std::ios::binary), fr(argv[3], std::ios::binary);
+        fl.read(reinterpret_cast<char *>(l.data), (std::streamsize)h * w);
+        fr.read(reinterpret_cast<char *>(r.data), (std::streamsize)h * w);
+        if (!fl || !fr) return 2;
+        using namespace sgm_amd;
+        GSGMPtr gsv = std::make_shared<GPU_SGM>(h, w, s, d);  // node.cpp:50
+        for (int frame = 0; frame < 2; ++frame) gsv->process(l, r);  // the handle is reused
+        const Mat &disp = gsv->get_disp();
+        std::ofstream fo(argv[8], std::ios::binary);
+        for (int i = 0; i < disp.rows; ++i)
+            fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)disp.cols * 4);
+        Mat view;
+        gsv->show_disp(view);
+        if (view.rows != 2 * (h / s) || view.cols != w / s) return 3;
+        std::ofstream fo2(argv[9], std::ios::binary);
+        for (int i = 0; i < disp.rows; ++i)
+            fo2.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)disp.cols * 4);
+        return fo && fo2 ? 0 : 4;
     }
     if (argc == 10 && std::string(argv[1]) == "runsky") {
         // process(l, r, sky, sky_beta) with either mask possibly "-" (empty);

@@ -81,6 +81,34 @@ def test_bm_class_surface_matches_oracle(exe, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scale,D", [(1, 64), (2, 64), (1, 128)])
+def test_gpu_sgm_class_matches_oracle(exe, tmp_path, scale, D):
+    # GPU_SGM (gpu_sgm/inc/SGM.cuh:23-62) built as node.cpp:50 would build it:
+    # the left view's sub-pixel map (SGM.cpp:32-443), post_filter()ed
+    # (GPU_SGM::process, gpu_sgm/src/SGM.cu:217-225), with the reference CPU
+    # semantics; show_disp() then marks the left d/s columns invalid in place
+    # (SGM.cu:238-246)
+    import oracle
+    oracle.build()
+    h, w = 90, 236
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=6)
+    fl, fr, fo, fo2 = (str(tmp_path / n) for n in ("l.raw", "r.raw", "out.raw", "out2.raw"))
+    left.tofile(fl)
+    right.tofile(fr)
+    r = subprocess.run([exe, "rungpu", fl, fr, str(h), str(w), str(scale), str(D), fo, fo2],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    H, W = h // scale, w // scale
+    got = np.fromfile(fo, dtype=np.float32).reshape(H, W)
+    sub = oracle.process(left, right, D, scale=scale, views=1)["sub"]
+    want = oracle.post_filter(sub, D, scale=scale)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    after = np.fromfile(fo2, dtype=np.float32).reshape(H, W)
+    want[:, :D // scale] = D + 1
+    assert np.array_equal(after.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_sky_detector_wrapper_matches_reference_example(exe, tmp_path):
     # sky_detector::SkyAreaDetector as node.cpp:51,83 uses it, on the
     # reference's own example (tests/golden/sky_000017_14.npz)
