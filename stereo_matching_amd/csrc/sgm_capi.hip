@@ -426,11 +426,14 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st, false,
                                          d_right, h->d_ct[1]);
            }));
-    HIPCHK(h, hipEventRecord(h->ev_ct, st));
+    // Events only where a second stream joins: on ROCm every event record in
+    // a stream costs the next kernel ~6 us of dispatch gap (measured, rocprof
+    // kernel trace), three of them per K128 frame before this was restricted.
     // two views on one stream: both DSIs + horizontal IIRs in one launch (a
     // view's H*D serial chains alone leave most SIMDs idle at KITTI sizes)
     const bool both_h = h->nviews == 2 && aux1 == st && (d_sky_l == nullptr) == (d_sky_r == nullptr) &&
                         sgm::cost_h2_supported(g, d_sky_l != nullptr);
+    if (h->nviews == 2 && !both_h && aux1 != st) HIPCHK(h, hipEventRecord(h->ev_ct, st));
     if (both_h) {
         HIPCHK(h, timed(h, "cost_h", 2.0 * npx * g.D, st, [&] {
                    return sgm::launch_cost_h2(h->d_ct[0], h->d_ct[1], d_sky_l, d_sky_r, sky_pitch, g,
@@ -440,15 +443,13 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         if ((rc = vfwd_view(h, 0, st)) != SGM_OK) return rc;
     } else {
         if (h->nviews == 2) {
-            HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
+            if (aux1 != st) HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
             if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
-            HIPCHK(h, hipEventRecord(h->ev_c[1], aux1));
         }
         if ((rc = cost_view(h, 0, right_only ? 1 : 0, right_only ? d_sky_r : d_sky_l, sky_pitch,
                             st)) != SGM_OK)
             return rc;
     }
-    HIPCHK(h, hipEventRecord(h->ev_c[0], st));
     // Volumes larger than the 256 MB Infinity Cache gain nothing from
     // finishing the left view first: both views' final passes then run as one
     // launch (fewer workgroup rounds at HD/4K)
@@ -470,8 +471,10 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         if (both_final)
             HIPCHK(h, timed(h, "pair_bwd_L4_final", 2.0 * npx * g.D, st,
                             [&] { return sgm::launch_final2(fin[0], fin[1], g, st); }));
-        HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
-        HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
+        if (aux1 != st) {
+            HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
+            HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
+        }
         HIPCHK(h, timed(h, "lr", npx, st, [&] {
                    return sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
                                          h->p.lr_max_diff, g, st);
@@ -655,8 +658,13 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1],
                              &h->ev_s[0], &h->ev_s[1], &h->ev_v1, &h->ev_pf,
                              &h->ev_last};
-        for (auto e : evs)
-            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { rc = SGM_ERR_HIP; break; }
+        for (auto e : evs) {
+            // stream-to-stream ordering on this device needs no system-scope
+            // fence (L2 writeback/invalidate); the post filter's host
+            // readback (ev_pf) keeps it
+            const unsigned fl = hipEventDisableTiming | (e == &h->ev_pf ? 0u : hipEventDisableSystemFence);
+            if (hipEventCreateWithFlags(e, fl) != hipSuccess) { rc = SGM_ERR_HIP; break; }
+        }
         if (rc) break;
         for (int v = 0; v < 2 && !rc; ++v) {
             if ((rc = dalloc(h, &h->d_in[v], nin))) break;
