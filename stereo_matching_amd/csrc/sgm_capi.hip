@@ -359,9 +359,9 @@ int vfwd_view(sgm_handle *h, int view, hipStream_t st) {
     return SGM_OK;
 }
 
-int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st);
+int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st, bool to_lk = false);
 int lk_refine(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
-              float *d_map, int map_pitch, hipStream_t st);
+              float *d_map, int map_pitch, hipStream_t st, bool staged = false);
 
 // BM::process (src/BM.cpp:9-97): census with BM's row decimation, the left
 // DSI + both cost filters (the vertical filter's fused L3 checkpoints are
@@ -487,10 +487,13 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     if (d_raw)
         HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
                                  hipMemcpyDeviceToDevice, st));
-    if (h->p.post_filter && (rc = post_filter(h, d_out, out_pitch, st)))  // SGM.cpp:821
+    // with LKRefine next, the post filter's last kernel writes LKRefine's
+    // input copy instead of the map (no device copy in between)
+    const bool pf_to_lk = h->p.post_filter && h->p.lk_refine;
+    if (h->p.post_filter && (rc = post_filter(h, d_out, out_pitch, st, pf_to_lk)))  // SGM.cpp:821
         return rc;
     if (h->p.lk_refine)  // SGM.cpp:824
-        return lk_refine(h, d_left, d_right, pitch, d_out, out_pitch, st);
+        return lk_refine(h, d_left, d_right, pitch, d_out, out_pitch, st, pf_to_lk);
     return SGM_OK;
 }
 
@@ -530,7 +533,9 @@ void pack_rows(uint8_t *dst, const uint8_t *src, size_t row_bytes, int rows, siz
 // convergence counter (the GPU keeps working through that round trip); in the
 // rare case the fill had not converged, more fill launches run and the
 // component kernels are enqueued again.
-int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
+// to_lk: write the filtered map to d_lk_in (contiguous) instead of d_map, for
+// lk_refine(..., staged = true) to read.
+int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st, bool to_lk) {
     const Geom g = h->g;
     const double dnpx = (double)g.H * g.W;
     float *F = h->d_pf_work;
@@ -550,7 +555,8 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
         // speckle_filter_new(filtered_disp, invalid_disp, SPECKLE_SIZE/scale, SPECKLE_DIS), :645
         HIPCHK(h, timed(h, "post_cc_apply", dnpx, st, [&] {
                    return sgm::launch_cc_apply(F, h->d_pf_label, h->d_pf_area, 1000 / g.scale,
-                                               (float)(g.D + 1), d_map, pitch, g, st);
+                                               (float)(g.D + 1), to_lk ? h->d_lk_in : d_map,
+                                               to_lk ? g.W : pitch, g, st);
                }));
         return SGM_OK;
     };
@@ -579,12 +585,14 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st) {
 
 // LKRefine (sgm_lk.hip) in place on a device map: the kernel reads a
 // contiguous copy of the map and writes the refined values back.
+// staged: d_lk_in already holds the map (post_filter(..., to_lk = true))
 int lk_refine(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
-              float *d_map, int map_pitch, hipStream_t st) {
+              float *d_map, int map_pitch, hipStream_t st, bool staged) {
     const Geom g = h->g;
     const size_t row = (size_t)g.W * sizeof(float);
-    HIPCHK(h, hipMemcpy2DAsync(h->d_lk_in, row, d_map, (size_t)map_pitch * sizeof(float), row, g.H,
-                               hipMemcpyDeviceToDevice, st));
+    if (!staged)
+        HIPCHK(h, hipMemcpy2DAsync(h->d_lk_in, row, d_map, (size_t)map_pitch * sizeof(float), row,
+                                   g.H, hipMemcpyDeviceToDevice, st));
     HIPCHK(h, timed(h, "lk_refine", (double)g.H * g.W, st, [&] {
                return sgm::launch_lk_refine(d_left, d_right, pitch, h->d_lk_in, d_map, map_pitch, g,
                                             st);

@@ -130,9 +130,11 @@ __global__ __launch_bounds__(256) void census_kernel(const uint8_t *__restrict__
                 if (di == HH && dj == HWW) continue;
                 // bit position k (0 = first, MSB) of the reference's order
                 const int k = di * (2 * HWW + 1) + dj - (di * (2 * HWW + 1) + dj > HH * (2 * HWW + 1) + HWW ? 1 : 0);
-                const unsigned bit = b[dj] > c[p] ? 1u : 0u;
-                if (k < NHI) hi[p] = (hi[p] << 1) | bit;
-                else lo[p] = (lo[p] << 1) | bit;
+                // (c - b) has its sign bit set iff b > c (bytes, no overflow):
+                // w << 1 | x >> 31 is one funnel shift (v_alignbit_b32)
+                const unsigned x = (unsigned)(c[p] - b[dj]);
+                if (k < NHI) hi[p] = (hi[p] << 1) | (x >> 31);
+                else lo[p] = (lo[p] << 1) | (x >> 31);
             }
         }
     }
