@@ -732,17 +732,24 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         const int half = wave - 2;
         const int px = lane / LPP, d0 = (lane - px * LPP) * QQ;
         const int slot = half * KP + px;
+        // T rows of chunk c: slot r is row H-1 - (cK + r).  Addressed from the
+        // chunk's top row (slot K-1; a wave-uniform pointer) plus this lane's
+        // constant byte offset; the partial last chunk's unused slots point
+        // into the volume's leading guard (kTGuardRows rows, never consumed).
+        const unsigned t_off = (unsigned)((((size_t)(K - 1 - slot) * W) * D + d0) * sizeof(float));
         auto tload = [&](float (&t)[QQ], int c) {
-            const int cnt = c == nseg - 1 ? r0 : K;
-            const int r = slot < cnt ? slot : 0;
-            const long long pix = (long long)(H - 1 - (c * K + r)) * W + path;
-            const float *src = a.acc_in + pix * D + d0;
+            const long long top = (long long)(H - K - c * K) * W + path;
+            const float *src = reinterpret_cast<const float *>(
+                reinterpret_cast<const char *>(a.acc_in + top * D) + t_off);
 #pragma unroll
             for (int k = 0; k < QQ; k += 4) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) t[k + e] = __builtin_nontemporal_load(src + k + e);
             }
         };
+        // results of chunk c: pixel (H-1 - cK - half*KP - px, path) = the
+        // wave's top pixel (px = KP-1) + (KP-1 - px) rows
+        const unsigned o_off = (unsigned)((KP - 1 - px) * W);
         // T for chunk c+2 is issued while chunk c is consumed (3 buffers)
         auto chunk = [&](const float (&t)[QQ], float (&tn)[QQ], int c) {
             tload(tn, c + 2 < nseg ? c + 2 : nseg - 1);
@@ -763,8 +770,8 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                 if (px < cnt) *reinterpret_cast<float4 *>(row + k) = x4;
             }
             wta_chunk_q<V, KP, QQ>(x, F->t[c & 1] + half * KP,
-                                   (long long)(H - 1 - c * K - half * KP) * W + path,
-                                   -(long long)W, cnt, lane, g.D, a.uniq, a.disp, a.sub);
+                                   (long long)(H - c * K - (half + 1) * KP) * W + path, o_off, cnt,
+                                   lane, g.D, a.uniq, a.disp, a.sub);
             bar();
         };
         float t0[QQ], t1[QQ], t2[QQ];

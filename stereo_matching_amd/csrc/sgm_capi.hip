@@ -43,6 +43,7 @@ struct sgm_handle {
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
     float *d_ch[2];       // horizontally filtered cost; reused as the T chain
+    float *d_ch_base[2];  // its allocation: d_ch is preceded by kTGuardRows rows (final pass)
     float *d_c[2];        // final cost volume
     float *d_s[2];        // S chain
     uint16_t *d_disp[2];  // WTA disparity
@@ -178,7 +179,7 @@ int dalloc(sgm_handle *h, T **p, size_t count) {
 void free_all(sgm_handle *h) {
     for (int v = 0; v < 2; ++v) {
         (void)hipFree(h->d_in[v]); (void)hipFree(h->d_sky[v]); (void)hipFree(h->d_ct[v]);
-        (void)hipFree(h->d_ch[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
+        (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
         (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
     }
     (void)hipFree(h->d_out);
@@ -680,7 +681,11 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if ((rc = dalloc(h, &h->d_ct[v], npx))) break;
         }
         for (int v = 0; v < (p->aux_only ? 0 : h->nviews) && !rc; ++v) {
-            if ((rc = dalloc(h, &h->d_ch[v], nvol))) break;
+            // the final pass addresses T chunks from their top row, which for
+            // the partial last chunk lies up to K-1 rows above row 0
+            const size_t guard = (size_t)sgm::t_guard_rows(h->g.D) * h->g.W * h->g.D;
+            if ((rc = dalloc(h, &h->d_ch_base[v], nvol + guard))) break;
+            h->d_ch[v] = h->d_ch_base[v] + guard;
             // + guard: the row-walking forward pass prefetches up to PF
             // positions past the end of the last row (never consumed)
             if ((rc = dalloc(h, &h->d_c[v], nvol + sgm::kVolGuard))) break;

@@ -579,10 +579,13 @@ __device__ __forceinline__ int group_min_i(int x) {
 // (SGM.cpp:383-408: the first strict minimum, the smallest other value and
 // its first index).
 // x: this lane's QQ total costs (disparities d0 .. d0+QQ-1 of pixel px); the
-// LDS rows tb[] hold the same totals for the sub-pixel's neighbours.
+// LDS rows tb[] hold the same totals for the sub-pixel's neighbours.  The
+// results go to pixel pix_top + pix_off: a wave-uniform index (SGPRs) plus
+// this lane's constant offset (>= 0), so the stores need no per-lane 64-bit
+// address arithmetic.
 template <int V, int PF, int QQ>
 __device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*tb)[tbuf_stride<V>()],
-                                            long long pix0, long long pix_step, int cnt, int lane,
+                                            long long pix_top, unsigned pix_off, int cnt, int lane,
                                             int Dn, float uniq, uint16_t *disp, float *sub) {
     constexpr int LPP = 64 / PF;  // lanes per pixel
     static_assert(QQ % 4 == 0 && LPP <= 32, "QQ a multiple of 4, at most 32 lanes per pixel");
@@ -624,9 +627,8 @@ __device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*
         f = (lim < xx) ? lim : xx;  // std::min(x, lim)
     }
     if (q == 0 && px < cnt) {
-        const long long pix = pix0 + px * pix_step;
-        disp[pix] = (uint16_t)d;
-        sub[pix] = f;
+        (disp + pix_top)[pix_off] = (uint16_t)d;
+        (sub + pix_top)[pix_off] = f;
     }
 }
 

@@ -12,6 +12,11 @@ namespace sgm {
 // read up to 64 positions (x D <= 256) past the last row's end.
 constexpr size_t kVolGuard = 64 * 256 + 256;
 
+// Rows of slack before the T volume read by the final pass (pair_split_body's
+// WTA waves load a chunk from its top row; the partial last chunk's top lies
+// up to K-1 rows above row 0, K = the vertical family's segment length).
+constexpr int t_guard_rows(int D) { return (D >= 256 ? 4 : 8) - 1; }
+
 // Geometry of one frame on the working (decimated) grid.
 struct Geom {
     int H, W, D;   // rows, cols, disparities
