@@ -136,6 +136,160 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
 #endif
 }
 
+// A diagonal cursor on the VALU: the same walk as Cursor<DIR> (wrapped
+// diagonals), with the column and offset held in VGPRs (wave-uniform values
+// the compiler is kept from moving to SGPRs).
+template <int DIR>
+struct VCursor {
+    int j, k;
+    long long off;
+    __device__ __forceinline__ void init(int path, int H, int W, int D, int lane) {
+        int z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // an opaque per-lane zero
+        (void)lane;
+        k = z;
+        j = path + z;
+        const int i = (DIR == 4 || DIR == 5) ? 0 : H - 1;
+        off = ((long long)i * W + j) * D;
+    }
+    __device__ __forceinline__ void advance(int W, long long D, long long WD) {
+        ++k;
+        if constexpr (DIR == 4 || DIR == 6) {
+            const bool wrap = j == W - 1;
+            off += (DIR == 4 ? WD : -WD) + (wrap ? -(long long)(W - 1) * D : D);
+            j = wrap ? 0 : j + 1;
+        } else {
+            const bool wrap = j == 0;
+            off += (DIR == 5 ? WD : -WD) + (wrap ? (long long)(W - 1) * D : -D);
+            j = wrap ? W - 1 : j - 1;
+        }
+    }
+    // advance only while k < n-1 (the load cursor stops on the last pixel)
+    __device__ __forceinline__ void advance_upto(int n, int W, long long D, long long WD) {
+        VCursor nx = *this;
+        nx.advance(W, D, WD);
+        const bool go = k < n - 1;
+        j = go ? nx.j : j;
+        off = go ? nx.off : off;
+        k = go ? nx.k : k;
+    }
+};
+
+// ------------------------------------------------- split diagonal sweeps
+//
+// The same sweep (diagonal DIR 4-7, MODE INIT or ACC) on two waves of one
+// workgroup: wave 0 moves memory -- the cost and accumulator rows of block
+// b+1 are loaded while block b is computed, written to an LDS ring, and the
+// results of block b-2 go back to global memory -- and wave 1 runs only the
+// DP, reading its inputs from and writing its outputs to LDS.  One LDS
+// barrier per block of BK steps.  A single wave interleaving the DP chain
+// with its own loads and stores reached 85% of the memory-only rate of the
+// same walk; the split reaches ~100% (tools/layout_probe.hip).
+template <int V, int BK>
+struct SweepSplitLds {
+    float c[3][BK][64 * V];  // costs
+    float a[3][BK][64 * V];  // acc_in rows (ACC)
+    float o[3][BK][64 * V];  // results
+};
+
+template <int DIR, int V, int MODE, bool FULL, int BK>
+__device__ __forceinline__ void sweep_split_body(const SweepArgs &a, const Geom &g, int path,
+                                                 SweepSplitLds<V, BK> &L) {
+    static_assert(DIR >= 4 && (MODE == SWEEP_INIT || MODE == SWEEP_ACC), "diagonal INIT/ACC sweeps");
+    constexpr bool NEED_ACC = MODE == SWEEP_ACC;
+    const int wave = wave_id();
+    const int lane = tid_x() & 63;
+    const int H = g.H, W = g.W;
+    const long long D = g.D, WD = (long long)g.W * g.D;
+    const int n = H;
+    const int nb = (n + BK - 1) / BK;
+    const int e0 = lane * V;
+    const bool active = FULL || e0 < g.D;
+    if (wave == 0) {
+        // ------------------------------------------------------ memory wave
+        // Addresses walk on the VALU (this wave's vector pipe is otherwise
+        // idle; scalar cursors here would compete with the DP waves' scalar
+        // work): VCursor keeps the column and the offset in VGPRs.
+        VCursor<DIR> pc, sc;  // next load, next store
+        pc.init(path, H, W, g.D, lane);
+        sc.init(path, H, W, g.D, lane);
+        float lc[BK][V], la[BK][V];
+        auto issue = [&] {
+#pragma unroll
+            for (int u = 0; u < BK; ++u) {
+                load_v<V>(lc[u], a.cost + pc.off + e0, active);
+                if (NEED_ACC) load_v_nt<V>(la[u], a.acc_in + pc.off + e0, active);
+                pc.advance_upto(n, W, D, WD);
+            }
+        };
+        issue();
+        for (int it = 0; it < nb + 2; ++it) {
+            if (it >= 2) {  // block it-2's results (written by the DP wave in iteration it-1)
+                const int b = it - 2;
+#pragma unroll
+                for (int u = 0; u < BK; ++u) {
+                    if (b * BK + u < n) {
+                        float o[V];
+                        load_lds_v<V>(o, &L.o[b % 3][u][e0]);
+                        store_v_nt<V>(a.acc_out + sc.off + e0, o, active);
+                        sc.advance(W, D, WD);
+                    }
+                }
+            }
+            if (it < nb) {
+#pragma unroll
+                for (int u = 0; u < BK; ++u) {
+                    store_lds_v<V>(&L.c[it % 3][u][e0], lc[u]);
+                    if (NEED_ACC) store_lds_v<V>(&L.a[it % 3][u][e0], la[u]);
+                }
+                if (it + 1 < nb) issue();
+            }
+            lds_barrier();
+        }
+    } else {
+        // --------------------------------------------------------- DP wave
+        __builtin_amdgcn_s_setprio(3);
+        const float p2v = to_vgpr(a.p2);
+        // the next step at which the wrapped chain meets the image edge and
+        // restarts (Cursor::start: DIR 4/6 wrap to column 0, DIR 5/7 to column
+        // W-1), then every W steps (frames taller than wide wrap repeatedly)
+        int kw = (DIR == 4 || DIR == 6) ? W - path : path + 1;
+        float prev[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+        float pmin = 0.0f;
+        for (int it = 0; it < nb + 2; ++it) {
+            if (it >= 1 && it - 1 < nb) {
+                const int b = it - 1;
+                // steps past the chain's end (the last block's tail) run on
+                // stale LDS slots; their results are never stored
+#pragma unroll
+                for (int u = 0; u < BK; ++u) {
+                    const int k = b * BK + u;
+                    {
+                        float c[V], ai[V], Lr[V];
+                        load_lds_v<V>(c, &L.c[b % 3][u][e0]);
+                        if (NEED_ACC) load_lds_v<V>(ai, &L.a[b % 3][u][e0]);
+                        dp_step<V>(prev, pmin, c, Lr, a.p1, p2v);
+                        const bool st = k == 0 || k == kw;
+                        kw = uniform(k == kw ? kw + W : kw);
+#pragma unroll
+                        for (int v = 0; v < V; ++v) Lr[v] = st ? c[v] : Lr[v];
+                        pmin = wave_min(lane_min(Lr));
+                        float o[V];
+#pragma unroll
+                        for (int v = 0; v < V; ++v) o[v] = NEED_ACC ? ai[v] + Lr[v] : Lr[v];
+                        store_lds_v<V>(&L.o[b % 3][u][e0], o);
+#pragma unroll
+                        for (int v = 0; v < V; ++v) prev[v] = Lr[v];
+                    }
+                }
+            }
+            lds_barrier();
+        }
+    }
+}
+
 // --------------------------------------------------------------- pairs
 //
 // Two opposite directions on the same scanlines (L1/L2 rows, L3/L4 columns,

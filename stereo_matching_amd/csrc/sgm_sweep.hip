@@ -16,6 +16,8 @@
 // Bit-exactness rules (DESIGN.md "Numerics"): built with -ffp-contract=off,
 // no fast-math, correctly rounded f32 division; every float expression keeps
 // the reference's association order.
+#include <cstdlib>
+
 #include "sgm_bodies.h"
 
 namespace sgm {
@@ -23,6 +25,24 @@ namespace sgm {
 template <int DIR, int V, int MODE, bool FULL, int PF>
 __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
     sweep_body<DIR, V, MODE, FULL, PF>(a, g, bid_x());
+}
+
+// Diagonal INIT/ACC sweeps (the L8 pass): memory wave + DP wave
+// (sweep_split_body), blocks of 4 steps.
+template <int DIR, int V, int MODE, bool FULL>
+__global__ __launch_bounds__(128) void sweep_split_kernel(SweepArgs a, Geom g) {
+    __shared__ __attribute__((aligned(16))) SweepSplitLds<V, 4> lds;
+    sweep_split_body<DIR, V, MODE, FULL, 4>(a, g, bid_x(), lds);
+}
+
+// The split sweep pays where the pass streams from HBM (a cost volume larger
+// than the 256 MB Infinity Cache: HD256 L8 1224 -> 1118 us); on a volume the
+// cache holds it is slower (K128 L8 114 -> 122 us).  SGM_SWEEP_SPLIT=0/1
+// forces it off/on (tests use it to cover both bodies at every size).
+static bool use_split_sweep(const Geom &g) {
+    const char *e = std::getenv("SGM_SWEEP_SPLIT");
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    return (size_t)g.H * g.W * g.D * sizeof(float) > (size_t(256) << 20);
 }
 
 // Steps of loads kept in flight: horizontal paths (few, long, latency-bound)
@@ -33,6 +53,19 @@ constexpr int sweep_pf() { return DIR < 2 ? 32 : 16; }
 template <int DIR, int MODE>
 static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(DIR < 2 ? g.H : g.W);
+    if constexpr (DIR >= 4 && MODE != SWEEP_STORE_L) {
+        if (use_split_sweep(g)) {
+            if (g.D == 32)
+                sweep_split_kernel<DIR, 1, MODE, false><<<grid, 128, 0, st>>>(a, g);
+            else if (g.D == 64)
+                sweep_split_kernel<DIR, 1, MODE, true><<<grid, 128, 0, st>>>(a, g);
+            else if (g.D == 128)
+                sweep_split_kernel<DIR, 2, MODE, true><<<grid, 128, 0, st>>>(a, g);
+            else
+                sweep_split_kernel<DIR, 4, MODE, true><<<grid, 128, 0, st>>>(a, g);
+            return;
+        }
+    }
     constexpr int PF = sweep_pf<DIR>();
     if (g.D == 32)
         sweep_kernel<DIR, 1, MODE, false, PF><<<grid, 64, 0, st>>>(a, g);

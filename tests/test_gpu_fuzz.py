@@ -4,7 +4,9 @@ scales), D, input kinds, sky masks, blur on/off, one or two views, and the
 SGM parameters the C-ABI exposes beyond the reference's constants -- P1, P2
 (SGM.cpp:27-28: 10, 100), the uniqueness ratio (inc/Solver.h:14: 0.7) and
 the LR threshold (inc/Solver.h:16: 1).  The oracle (oracle/sgm_oracle.c)
-takes the same parameters."""
+takes the same parameters.  Every case runs with both bodies of the diagonal
+L8 sweep (SGM_SWEEP_SPLIT: the one-wave sweep and the memory-wave + DP-wave
+split, which the library picks by volume size)."""
 from __future__ import annotations
 
 import numpy as np
@@ -40,7 +42,9 @@ CASES = [_case(k) for k in range(N_CASES)]
     f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_P{c['p1']}-{c['p2']}_u{c['uniq']}_lr{c['lr']}"
     f"_{c['kind']}{'_sky' if c['sky'] else ''}{'' if c['blur'] else '_noblur'}_V{c['views']}"
     for c in CASES])
-def test_random_frame(c):
+@pytest.mark.parametrize("split", ["0", "1"], ids=["onewave", "split"])
+def test_random_frame(c, split, monkeypatch):
+    monkeypatch.setenv("SGM_SWEEP_SPLIT", split)
     h, w, D, s = c["h"], c["w"], c["D"], c["s"]
     left, right = synthetic.stereo_pair(h, w, D, pair_index=100 + c["seed"], kind=c["kind"])
     H, W = h // s, w // s
