@@ -62,23 +62,37 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
     const int e0 = lane * V;
     const bool active = FULL || e0 < g.D;
     constexpr bool NEED_ACC = MODE == SWEEP_ACC;
+    // band: steps [kb, ke) (backward diagonals only; others run whole chains)
+    constexpr bool BANDED = DIR >= 6;
+    const int kb = BANDED ? a.band.kb : 0;
+    const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
 
     Cursor<DIR> cc, pc;
-    cc.init(path, H, W, g.D);
-    pc.init(path, H, W, g.D);
+    if (BANDED) {
+        cc.init_at(path, kb, H, W, g.D);
+        pc.init_at(path, kb, H, W, g.D);
+    } else {
+        cc.init(path, H, W, g.D);
+        pc.init(path, H, W, g.D);
+    }
 
     float cb[PF][V], ab[PF][V];
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
         load_v<V>(cb[u], a.cost + pc.off + e0, active);
         if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
-        pc.advance_upto(n, W, D, WD);
+        pc.advance_upto(ke, W, D, WD);
     }
 
     float prev[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
     float pmin = 0.0f;
+    if (BANDED && kb > 0) {  // the chain state entering the band
+        load_v<V>(prev, a.band.carry + (size_t)path * g.D + e0, active);
+        pmin = wave_min(lane_min(prev));
+    } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = SGM_INF;
+    }
 
     // One DP step on ring slot u; branch-free so the waitcnt pass can keep
     // exact counts (each slot's loads are waited for PF steps later).
@@ -119,18 +133,19 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
             // the new load lands in the same registers (no copy, no wait)
             load_v<V>(cb[u], a.cost + pc.off + e0, active);
             if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
-            pc.advance_upto(n, W, D, WD);
+            pc.advance_upto(ke, W, D, WD);
         }
     };
 
-    int k0 = 0;
-    for (; k0 + PF <= n; k0 += PF) {
+    int k0 = kb;
+    for (; k0 + PF <= ke; k0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) step(u, true);
     }
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        if (k0 + u < n) step(u, false);
+        if (k0 + u < ke) step(u, false);
+    if (BANDED && ke < n) store_v<V>(a.band.carry + (size_t)path * g.D + e0, prev, active);
 #ifdef SGM_STAMPS
     stamp_flush(DIR == 4 ? 8 : (DIR == 7 ? 9 : 10), st_t0);
 #endif
@@ -432,6 +447,13 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     const int r0 = n - (nseg - 1) * K;
     const int e0 = lane * V;
     const bool active = FULL || e0 < g.D;
+    // band (PAIR_D2 ACC, the frame schedule's stage B): backward steps
+    // [kb, ke) = segments s_lo .. s_hi (backward step block c is segment
+    // nseg-1-c)
+    constexpr bool BANDED = FAM == PAIR_D2 && MODE == PAIR_ACC;
+    const int kb = BANDED ? a.band.kb : 0;
+    const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
+    const int s_hi = nseg - 1 - kb / K, s_lo = nseg - (ke + K - 1) / K;
 
     if constexpr (FINAL) {
         if (wave == 1) {  // WTA consumer, one chunk per segment
@@ -451,21 +473,31 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     const float *ck = a.ckpt + (size_t)path * nseg * g.D + e0;
 
     Cursor<BD> bc, pc;
-    bc.init(bpath, H, W, g.D);
-    pc.init(bpath, H, W, g.D);
+    if (BANDED) {
+        bc.init_at(bpath, kb, H, W, g.D);
+        pc.init_at(bpath, kb, H, W, g.D);
+    } else {
+        bc.init(bpath, H, W, g.D);
+        pc.init(bpath, H, W, g.D);
+    }
     float ab[K][V], sb[K][V];
 #pragma unroll
     for (int u = 0; u < K; ++u) {
         if (NEED_ACC) load_v_nt<V>(ab[u], a.acc_in + pc.off + e0, active);
         if (NEED_S) load_v_nt<V>(sb[u], a.s_in + pc.off + e0, active);
-        pc.advance_upto(n, W, D, WD);
+        pc.advance_upto(ke, W, D, WD);
     }
 
     float c0[K + 1][V], c1[K + 1][V], lf[K][V];
     float prevb[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
     float pminb = 0.0f;
+    if (BANDED && kb > 0) {  // the chain state entering the band
+        load_v<V>(prevb, a.band.carry + (size_t)path * g.D + e0, active);
+        pminb = wave_min(lane_min(prevb));
+    } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) prevb[v] = SGM_INF;
+    }
 
     // costs of segment s into cs; array slot kk holds position
     // pos0 + kk - (K - cnt) (slots below K - cnt are unused for the partial
@@ -555,7 +587,7 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
                 bc.advance(W, D, WD);
                 if (NEED_ACC) load_v_nt<V>(ab[r], a.acc_in + pc.off + e0, active);
                 if (NEED_S) load_v_nt<V>(sb[r], a.s_in + pc.off + e0, active);
-                pc.advance_upto(n, W, D, WD);
+                pc.advance_upto(ke, W, D, WD);
             }
         }
         if (FINAL) lds_barrier();
@@ -566,21 +598,27 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     // segment), then segment 0, which may be partial.
     using full_t = std::integral_constant<bool, true>;
     using part_t = std::integral_constant<bool, false>;
-    load_seg(c0, nseg - 1);
-    int s = nseg - 1;
-    for (; s >= 2; s -= 2) {
+    // (a band ending above segment 0 ends on a full segment)
+    auto last = [&](float (&cs)[K + 1][V]) {
+        if (s_lo == 0) process_seg(cs, 0, part_t{});
+        else process_seg(cs, s_lo, full_t{});
+    };
+    load_seg(c0, s_hi);
+    int s = s_hi;
+    for (; s >= s_lo + 2; s -= 2) {
         load_seg(c1, s - 1);
         process_seg(c0, s, full_t{});
         load_seg(c0, s - 2);
         process_seg(c1, s - 1, full_t{});
     }
-    if (s == 1) {
-        load_seg(c1, 0);
-        process_seg(c0, 1, full_t{});
-        process_seg(c1, 0, part_t{});
+    if (s == s_lo + 1) {
+        load_seg(c1, s_lo);
+        process_seg(c0, s_lo + 1, full_t{});
+        last(c1);
     } else {
-        process_seg(c0, 0, part_t{});
+        last(c0);
     }
+    if (BANDED && ke < n) store_v<V>(a.band.carry + (size_t)path * g.D + e0, prevb, active);
     if (FINAL) lds_barrier();
 #ifdef SGM_STAMPS
     stamp_flush(FAM == PAIR_D2 ? 11 : (FAM == PAIR_H ? 13 : 14), st_t0);
@@ -664,6 +702,13 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     constexpr bool LIN = FAM != PAIR_D2;
     const long long lin_base = FAM == PAIR_H ? (long long)path * WD : (long long)path * D;
     const long long lin_st = FAM == PAIR_H ? D : WD;
+    // band (PAIR_V): backward steps [kb, ke) = chunks [c_lo, c_hi) = segments
+    // s_lo .. s_hi (chunk c is segment nseg-1-c)
+    constexpr bool BANDED = FAM == PAIR_V;
+    const int kb = BANDED ? a.band.kb : 0;
+    const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
+    const int c_lo = kb / K, c_hi = (ke + K - 1) / K;
+    const int s_hi = nseg - 1 - c_lo, s_lo = nseg - c_hi;
 
     if (wave == 0) {
         // H rows: the recompute chain is the slower one; V: the backward one
@@ -677,7 +722,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         // costs so recomputation never waits on a load younger than the
         // look-ahead
         auto load_seg = [&](float (&cs)[K + 1][V], int s) {
-            s = s < 0 ? 0 : s;
+            s = s < s_lo ? s_lo : s;
             const int cnt = s == 0 ? r0 : K;
             const int pos0 = s == 0 ? 0 : r0 + (s - 1) * K;
             if constexpr (LIN) {
@@ -738,13 +783,13 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             }
             bar();
         };
-        // buffer u holds segment nseg-1-m for m = u (mod NB)
+        // buffer u holds segment s_hi-m for m = u (mod NB)
 #pragma unroll
-        for (int u = 0; u + 1 < NB; ++u) load_seg(cb[u], nseg - 1 - u);
-        int s = nseg - 1;
+        for (int u = 0; u + 1 < NB; ++u) load_seg(cb[u], s_hi - u);
+        int s = s_hi;
         // full segments NB at a time, each step first issuing the segment
         // NB-1 further down
-        for (; s - (NB - 1) >= 1; s -= NB) {
+        for (; s - (NB - 1) >= s_lo + 1; s -= NB) {
 #pragma unroll
             for (int u = 0; u < NB; ++u) {
                 load_seg(cb[(u + NB - 1) % NB], s - u - (NB - 1));
@@ -755,7 +800,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         auto tail = [&](auto u_tag) {
             constexpr int U = decltype(u_tag)::value;
             if constexpr (U < NB) {
-                if (s >= 1) {
+                if (s >= s_lo + 1) {
                     load_seg(cb[(U + NB - 1) % NB], s - (NB - 1));
                     produce(cb[U], s, full_t{});
                     --s;
@@ -764,11 +809,15 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         };
         tail(std::integral_constant<int, 0>{});
         if constexpr (NB == 3) tail(std::integral_constant<int, 1>{});
-        // segment 0 is in buffer (nseg - 1) % NB
-        const int b0 = (nseg - 1) % NB;
-        if (b0 == 0) produce(cb[0], 0, part_t{});
-        else if (b0 == 1) produce(cb[1], 0, part_t{});
-        else produce(cb[NB - 1], 0, part_t{});
+        // segment s_lo is in buffer (s_hi - s_lo) % NB; only segment 0 is partial
+        const int b0 = (s_hi - s_lo) % NB;
+        auto last = [&](auto tag) {
+            if (b0 == 0) produce(cb[0], s_lo, tag);
+            else if (b0 == 1) produce(cb[1], s_lo, tag);
+            else produce(cb[NB - 1], s_lo, tag);
+        };
+        if (!BANDED || s_lo == 0) last(part_t{});
+        else last(full_t{});
 #pragma unroll
         for (int t = 0; t < NSTAGE - 1; ++t) bar();
     } else if (wave == 1) {
@@ -782,8 +831,8 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         pc.init(bpath, H, W, g.D);
         // LIN: running offsets of the step (bo) and of the ring refill (po,
         // position pp, held at position 0 past the chain's end)
-        long long bo = lin_base + (long long)(n - 1) * lin_st, po = bo;
-        int pp = n - 1;
+        long long bo = lin_base + (long long)(n - 1 - kb) * lin_st, po = bo;
+        int pp = n - 1 - kb;
         auto padv = [&] {
             if constexpr (LIN) {
                 po -= pp > 0 ? lin_st : 0;
@@ -801,9 +850,14 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             padv();
         }
         float prevb[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) prevb[v] = LIN ? 0.0f : SGM_INF;
         float pminb = 0.0f;
+        if (BANDED && kb > 0) {  // the chain state entering the band
+            load_v<V>(prevb, a.band.carry + (size_t)path * g.D + e0, active);
+            pminb = wave_min(lane_min(prevb));
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v) prevb[v] = LIN ? 0.0f : SGM_INF;
+        }
         auto consume = [&](int c, auto full_tag, auto half_tag) {
             constexpr bool FULLSEG = decltype(full_tag)::value;
             constexpr int HF = decltype(half_tag)::value;
@@ -859,17 +913,18 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         using h0 = std::integral_constant<int, 0>;
         using h1 = std::integral_constant<int, RH - 1>;
         bar();
-        int c = 0;
-        for (; c + RH <= nseg - 1; c += RH) {
+        int c = c_lo;
+        for (; c + RH <= c_hi - 1; c += RH) {
             consume(c, full_t{}, h0{});
             if constexpr (RH == 2) consume(c + 1, full_t{}, h1{});
         }
-        if (RH == 2 && c < nseg - 1) {
+        if (RH == 2 && c < c_hi - 1) {
             consume(c, full_t{}, h0{});
             consume(c + 1, part_t{}, h1{});
         } else {
             consume(c, part_t{}, h0{});
         }
+        if (BANDED && ke < n) store_v<V>(a.band.carry + (size_t)path * g.D + e0, prevb, active);
         if (FINAL) bar();
     } else if constexpr (FINAL) {
         __builtin_amdgcn_s_setprio(3);  // the WTA wave is the slowest stage of the final pipeline
@@ -906,7 +961,7 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         const unsigned o_off = (unsigned)((KP - 1 - px) * W);
         // T for chunk c+2 is issued while chunk c is consumed (3 buffers)
         auto chunk = [&](const float (&t)[QQ], float (&tn)[QQ], int c) {
-            tload(tn, c + 2 < nseg ? c + 2 : nseg - 1);
+            tload(tn, c + 2 < c_hi ? c + 2 : c_hi - 1);
             const int cnt_all = c == nseg - 1 ? r0 : K;
             const int cnt = cnt_all - half * KP < 0 ? 0 : (cnt_all - half * KP > KP ? KP : cnt_all - half * KP);
             // total = X + T in registers (the WTA's own lane layout); the row
@@ -929,18 +984,18 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
             bar();
         };
         float t0[QQ], t1[QQ], t2[QQ];
-        tload(t0, 0);
-        tload(t1, nseg > 1 ? 1 : 0);
+        tload(t0, c_lo);
+        tload(t1, c_lo + 1 < c_hi ? c_lo + 1 : c_lo);
         bar();
         bar();
-        int c = 0;
-        for (; c + 2 < nseg; c += 3) {
+        int c = c_lo;
+        for (; c + 2 < c_hi; c += 3) {
             chunk(t0, t2, c);
             chunk(t1, t0, c + 1);
             chunk(t2, t1, c + 2);
         }
-        if (c < nseg) chunk(t0, t2, c);
-        if (c + 1 < nseg) chunk(t1, t0, c + 1);
+        if (c < c_hi) chunk(t0, t2, c);
+        if (c + 1 < c_hi) chunk(t1, t0, c + 1);
     }
 #ifdef SGM_STAMPS
     if (lane == 0) {

@@ -52,6 +52,8 @@ struct sgm_handle {
     float *d_min;         // minL (stage_path)
     float *d_zero;        // 256 zero floats (PairArgs::zero)
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
+    float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
+    int band_rows;        // rows per band of the backward phase (0: whole volume)
     // post_filter scratch (sgm_post.hip)
     float *d_pf_orig;     // the map as it entered the median fill
     float *d_pf_work;     // contiguous working map (pitched callers)
@@ -180,6 +182,7 @@ void free_all(sgm_handle *h) {
     for (int v = 0; v < 2; ++v) {
         (void)hipFree(h->d_in[v]); (void)hipFree(h->d_sky[v]); (void)hipFree(h->d_ct[v]);
         (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
+        for (auto &c : h->d_carry[v]) (void)hipFree(c);
         (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
     }
     (void)hipFree(h->d_out);
@@ -286,6 +289,32 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
                  [&] { return sgm::launch_pair_bwd(fam, mode, a, h->g, st); });
 }
 
+// Rows per band of the backward phase (stage B's diagonal pair, the L8
+// sweep, the final pass) for cost volumes above the 256 MB Infinity Cache:
+// about 192 MB of cost volume per band, so that a band's C and T stay in the
+// cache from one pass to the next (tools/band_probe.hip: 1.27-1.35x for the
+// three passes' streams alone; in the frame HD256 -3.5%, 4K256 -5%; 94-126 MB
+// bands gain less).  A volume the cache already holds (K128) loses by it.
+// Band edges sit on multiples of 16 rows from the bottom: whole segments of
+// every pair family.
+// SGM_BAND_ROWS overrides (0: whole-volume passes).
+int band_rows_for(Geom g) {
+    const char *e = getenv("SGM_BAND_ROWS");
+    const double row_bytes = (double)g.W * g.D * sizeof(float);
+    int rows;
+    if (e && *e) {
+        rows = atoi(e);
+    } else {
+#ifdef SGM_NO_BANDS
+        return 0;
+#endif
+        if (row_bytes * g.H <= 256.0 * 1024 * 1024) return 0;
+        rows = (int)(192.0 * 1024 * 1024 / row_bytes);
+    }
+    rows -= rows % 16;
+    return rows <= 0 || rows >= g.H ? 0 : rows;
+}
+
 // The 8-path aggregation of one view, given the final cost volume and the L3
 // checkpoints (written by vfwd, or by the PAIR_V forward pass here when
 // `need_v_ckpt`), as three launches on one stream:
@@ -317,18 +346,38 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     h2.out = S;
     d7.acc_in = T;
     d7.out = T;
-    HIPCHK(h, timed(h, "stage_b", elems, st,
-                    [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
+    const int H = h->g.H, BR = h->band_rows;
+    if (BR == 0 || defer_final)
+        HIPCHK(h, timed(h, "stage_b", elems, st,
+                        [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
     SweepArgs l8 = sweep_args(h);
     l8.cost = cost;
     l8.acc_in = T;
     l8.acc_out = T;
-    HIPCHK(h, sweep(h, SGM_DIR_L8, sgm::SWEEP_ACC, l8, st));
     pa.ckpt = ck[sgm::PAIR_V];
     pa.s_in = S;
     pa.acc_in = T;
     pa.disp = disp;
     pa.sub = sub;
+    if (BR > 0 && !defer_final) {
+        // bottom band first: the backward passes walk up
+        for (int kb = 0; kb < H; kb += BR) {
+            const int ke = kb + BR < H ? kb + BR : H;
+            const double be = (double)(ke - kb) / H * elems;
+            d7.band = {kb, ke, h->d_carry[view][0]};
+            HIPCHK(h, timed(h, "stage_b", be, st,
+                            [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
+            l8.band = {kb, ke, h->d_carry[view][1]};
+            pa.band = {kb, ke, h->d_carry[view][2]};
+            HIPCHK(h, timed(h, "sweep_L8_acc", be, st,
+                            [&] { return sgm::launch_sweep(SGM_DIR_L8, sgm::SWEEP_ACC, l8, h->g, st); }));
+            HIPCHK(h, timed(h, "pair_bwd_L4_final", be, st, [&] {
+                       return sgm::launch_pair_bwd(sgm::PAIR_V, sgm::PAIR_FINAL, pa, h->g, st);
+                   }));
+        }
+        return SGM_OK;
+    }
+    HIPCHK(h, sweep(h, SGM_DIR_L8, sgm::SWEEP_ACC, l8, st));
     if (defer_final) {  // the caller launches this view's final pass with the other view's
         *defer_final = pa;
         return SGM_OK;
@@ -454,7 +503,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // Volumes larger than the 256 MB Infinity Cache gain nothing from
     // finishing the left view first: both views' final passes then run as one
     // launch (fewer workgroup rounds at HD/4K)
-    const bool both_final = h->nviews == 2 && aux1 == st &&
+    const bool both_final = h->nviews == 2 && aux1 == st && h->band_rows == 0 &&
                             (double)g.H * g.W * g.D * sizeof(float) > 256.0 * 1024 * 1024 &&
                             !getenv("SGM_SPLIT_FINAL");
     sgm::PairArgs fin[2];
@@ -694,7 +743,10 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if ((rc = dalloc(h, &h->d_sub[v], npx))) break;
             for (int f = 0; f < 3 && !rc; ++f)
                 rc = dalloc(h, &h->d_ck[v][f], sgm::pair_ckpt_floats(f, h->g));
+            for (int f = 0; f < 3 && !rc; ++f)
+                rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D);
         }
+        h->band_rows = band_rows_for(h->g);
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {
                 if ((rc = dalloc(h, &h->d_disp[v], npx))) break;

@@ -185,14 +185,19 @@ struct Cursor {
         else { i = H - 1; j = path; }
         off = ((long long)i * W + j) * D;
     }
-    // Position the cursor at step k of chain `path` (forward directions only:
-    // L1 row walk, L3 column walk, L5 / L6 wrapped diagonals).
+    // Position the cursor at step k of chain `path` (L1 row walk, L3 column
+    // walk, L5 / L6 wrapped diagonals; the backward walks L2, L4, L7, L8 for
+    // bands).
     __device__ __forceinline__ void init_at(int path, int kk, int H, int W, int D) {
         k = kk;
         if (DIR == 0) { i = path; j = kk; }
+        else if (DIR == 1) { i = path; j = W - 1 - kk; }
         else if (DIR == 2) { i = kk; j = path; }
+        else if (DIR == 3) { i = H - 1 - kk; j = path; }
         else if (DIR == 4) { i = kk; j = uniform((path + kk) % W); }
-        else { i = kk; j = uniform(((path - kk) % W + W) % W); }  // DIR 5
+        else if (DIR == 5) { i = kk; j = uniform(((path - kk) % W + W) % W); }
+        else if (DIR == 6) { i = H - 1 - kk; j = uniform((path + kk) % W); }
+        else { i = H - 1 - kk; j = uniform(((path - kk) % W + W) % W); }  // DIR 7
         off = ((long long)i * W + j) * D;
     }
     __device__ __forceinline__ bool start(int W) const {

@@ -31,6 +31,18 @@ enum SweepMode {
     SWEEP_FINAL = 3     // (retired: the final pass is the PAIR_V backward kernel)
 };
 
+// A band of a backward pass: chain steps [kb, ke) of every chain (the rows
+// H-ke .. H-1-kb of the walks that start at the bottom row), the chain state
+// entering the band read from carry (kb > 0) and the state leaving it written
+// there (ke < chain length; carry holds D floats per chain).  ke = 0: the
+// whole chain.  The backward phase (stage B's diagonal pair, L8, final) runs
+// band by band above the Infinity Cache, so that a band's cost volume and T
+// stay cached from one pass to the next (DESIGN.md "Bands").
+struct Band {
+    int kb, ke;
+    float *carry;
+};
+
 struct SweepArgs {
     const float *cost;   // HWD
     const float *acc_in; // HWD (ACC: chain state; FINAL: T chain)
@@ -40,6 +52,7 @@ struct SweepArgs {
     uint16_t *disp;      // HW  (FINAL)
     float *sub;          // HW  (FINAL)
     float p1, p2, uniq;
+    Band band;           // backward diagonal sweeps (DIR 6, 7: the L8 pass)
 };
 
 // Scanline families fused into forward/backward pairs (DESIGN.md "Pairs"):
@@ -68,6 +81,7 @@ struct PairArgs {
     const float *zero;   // >= 256 zero floats: the cost of the virtual positions
                          // that align forward passes with their checkpoints
     float p1, p2, uniq;
+    Band band;           // backward passes (D2 ACC, V FINAL): steps in whole segments
 };
 
 // floats of checkpoint storage a family needs

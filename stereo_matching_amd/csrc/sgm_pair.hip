@@ -200,16 +200,24 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
 // Stage B blocks are two waves: an H block splits its row's L2 pass into a
 // recompute wave and a backward wave (pair_split_body); a D2 block runs two
 // anti-diagonal L7 chains, one per wave.
+// A banded stage B (d7.band: the diagonal pair's steps [kb, ke)) runs the H
+// rows -- whole-row chains, the launch's critical path -- only with the first
+// band.
+__host__ __device__ inline int stage_b_rows(const PairArgs &d7, const Geom &g) {
+    return d7.band.ke > 0 && d7.band.kb > 0 ? 0 : g.H;
+}
+
 template <int V, bool FULL>
 __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
     constexpr int K = pair_k<V>();
     __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
     const int b = bid_x(), wave = wave_id();
-    if (b < g.H) {
+    const int nh = stage_b_rows(d7, g);
+    if (b < nh) {
         pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K, 3>(h2, g, b, wave, lds, nullptr);
         return;
     }
-    const int path = 2 * (b - g.H) + wave;
+    const int path = 2 * (b - nh) + wave;
     if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(d7, g, path, nullptr, nullptr);
 }
 
@@ -224,7 +232,7 @@ hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArg
 }
 
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st) {
-    const dim3 grid(g.H + (g.W + 1) / 2);
+    const dim3 grid(stage_b_rows(d7, g) + (g.W + 1) / 2);
     if (g.D == 32) stage_b_kernel<1, false><<<grid, 128, 0, st>>>(h2, d7, g);
     else if (g.D == 64) stage_b_kernel<1, true><<<grid, 128, 0, st>>>(h2, d7, g);
     else if (g.D == 128) stage_b_kernel<2, true><<<grid, 128, 0, st>>>(h2, d7, g);

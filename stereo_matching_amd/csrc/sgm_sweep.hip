@@ -54,7 +54,7 @@ template <int DIR, int MODE>
 static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(DIR < 2 ? g.H : g.W);
     if constexpr (DIR >= 4 && MODE != SWEEP_STORE_L) {
-        if (use_split_sweep(g)) {
+        if (a.band.ke == 0 && use_split_sweep(g)) {  // (banded sweeps: the one-wave body)
             if (g.D == 32)
                 sweep_split_kernel<DIR, 1, MODE, false><<<grid, 128, 0, st>>>(a, g);
             else if (g.D == 64)

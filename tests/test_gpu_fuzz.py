@@ -6,7 +6,8 @@ SGM parameters the C-ABI exposes beyond the reference's constants -- P1, P2
 the LR threshold (inc/Solver.h:16: 1).  The oracle (oracle/sgm_oracle.c)
 takes the same parameters.  Every case runs with both bodies of the diagonal
 L8 sweep (SGM_SWEEP_SPLIT: the one-wave sweep and the memory-wave + DP-wave
-split, which the library picks by volume size)."""
+split, which the library picks by volume size), and once more with the
+backward phase in bands (SGM_BAND_ROWS)."""
 from __future__ import annotations
 
 import numpy as np
@@ -45,6 +46,19 @@ CASES = [_case(k) for k in range(N_CASES)]
 @pytest.mark.parametrize("split", ["0", "1"], ids=["onewave", "split"])
 def test_random_frame(c, split, monkeypatch):
     monkeypatch.setenv("SGM_SWEEP_SPLIT", split)
+    _check(c)
+
+
+@pytest.mark.parametrize("c", CASES, ids=[f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_V{c['views']}" for c in CASES])
+def test_random_frame_banded(c, monkeypatch):
+    """The backward phase in 16-row bands (the schedule of volumes above the
+    Infinity Cache: stage B's diagonal pair, L8 and the final pass band by
+    band, chain states carried across band edges)."""
+    monkeypatch.setenv("SGM_BAND_ROWS", "16")
+    _check(c)
+
+
+def _check(c):
     h, w, D, s = c["h"], c["w"], c["D"], c["s"]
     left, right = synthetic.stereo_pair(h, w, D, pair_index=100 + c["seed"], kind=c["kind"])
     H, W = h // s, w // s

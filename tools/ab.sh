@@ -1,7 +1,7 @@
 #!/bin/bash
 # Paired A/B timing of library builds on one box: bench.py alternates
 # between the libraries REPS times (SGM_HIP_LIB), printing MPD/s and the
-# per-kernel event times of every run.  Usage (GPU box):
+# per-kernel event time per step (us) of every run.  Usage (GPU box):
 #   bash tools/ab.sh CONFIG REPS LIB_A LIB_B [LIB_C ...]
 set -o pipefail
 CFG=$1; REPS=$2; shift 2
@@ -12,6 +12,6 @@ for r in $(seq 1 $REPS); do
       > gpurun_out/ab_last.json 2>> gpurun_out/ab.err || { echo "bench failed for $L"; tail -20 gpurun_out/ab.err; exit 1; }
     python -c "
 import json; r=json.loads(open('gpurun_out/ab_last.json').read().strip().splitlines()[-1])
-print('%-28s %9.1f MPD/s %7.4f ms  ' % ('$L'[-28:], r['value'], r['ms_per_step']) + ' '.join('%s=%.1f' % (k[:10], v['avg_us']) for k, v in r['kernels'].items()))"
+print('%-28s %9.1f MPD/s %7.4f ms  ' % ('$L'[-28:], r['value'], r['ms_per_step']) + ' '.join('%s=%.1f' % (k[:10], v['share_per_step_ms'] * 1e3) for k, v in r['kernels'].items()))"
   done
 done

@@ -71,7 +71,7 @@ static double run(int H, int W, int D, int band_rows, float *C, float *T5, float
 
 int main() {
     struct Cfg { const char *name; int H, W, D; };
-    for (Cfg cfg : {Cfg{"4K256", 2160, 3840, 256}, Cfg{"HD256", 1080, 1920, 256}}) {
+    for (Cfg cfg : {Cfg{"K128", 375, 1242, 128}, Cfg{"4K256", 2160, 3840, 256}, Cfg{"HD256", 1080, 1920, 256}}) {
         const long long n = (long long)cfg.H * cfg.W * cfg.D;
         float *C, *T5, *S12, *T, *sink;
         if (hipMalloc(&C, n * 4) || hipMalloc(&T5, n * 4) || hipMalloc(&S12, n * 4) || hipMalloc(&T, n * 4) ||
