@@ -340,13 +340,17 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     SweepArgs l5 = sweep_args(h);
     l5.cost = cost;
     l5.acc_out = T;
-    HIPCHK(h, timed(h, "stage_a", elems, st,
-                    [&] { return sgm::launch_stage_a(h1, l5, d6, h->g, st); }));
     sgm::PairArgs h2 = h1, d7 = d6;
     h2.out = S;
     d7.acc_in = T;
     d7.out = T;
     const int H = h->g.H, BR = h->band_rows;
+    // banded: stage A runs the whole H pair (S12), stage B's bands only the
+    // diagonal pair
+    const bool banded = BR > 0 && !defer_final;
+    HIPCHK(h, timed(h, "stage_a", elems, st, [&] {
+               return sgm::launch_stage_a(h1, l5, d6, h->g, st, banded ? &h2 : nullptr);
+           }));
     if (BR == 0 || defer_final)
         HIPCHK(h, timed(h, "stage_b", elems, st,
                         [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));

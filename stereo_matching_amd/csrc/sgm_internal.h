@@ -94,8 +94,10 @@ hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStre
 // in = horizontally filtered volume, out = final cost volume, a.ckpt = L3
 // checkpoints.
 // Multi-role launches of the frame schedule (sgm_pair.hip).
+// h2 (the banded schedule): stage A also runs the H pair's backward half
+// into h2.out, and banded stage B launches (d7.band) run no H rows
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
-                          hipStream_t st);
+                          hipStream_t st, const PairArgs *h2 = nullptr);
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st);
 hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st);
 

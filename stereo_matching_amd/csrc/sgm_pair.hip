@@ -178,15 +178,25 @@ __global__ __launch_bounds__(256) void pair_final2_kernel(PairArgs a0, PairArgs 
 // H blocks come first so they start at once.
 //   stage A: L1 forward (ckpt)  |  L5 -> T5         |  L6 forward (ckpt)
 //   stage B: L2 backward -> S12 |  L7 backward: T = (T5 + L6) + L7
-template <int V, bool FULL>
+// HP (the banded schedule, volumes above the Infinity Cache): an H block
+// also runs its row's backward half (L2 recomputing L1 from the checkpoints
+// it has just written -> S12), so that the banded stage B launches carry no
+// whole-row chains.  (Two-wave blocks running the backward half split over
+// both waves, as stage B does, were slower: the split's LDS ring on every
+// block of the launch cuts the diagonal roles' occupancy.)
+template <int V, bool FULL, bool HP>
 __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, PairArgs d6,
-                                                     Geom g) {
+                                                     PairArgs h2, Geom g) {
     constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
     int b = bid_x();
     if (b < g.H) {
         // the H chains (few, long) are the launch's critical path
         __builtin_amdgcn_s_setprio(3);
         pair_fwd_body<0, V, FULL, PFH>(h1, g, b);
+        if constexpr (HP) {
+            __threadfence();  // this wave's checkpoint stores, before it reads them back
+            pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, b, nullptr, nullptr);
+        }
         return;
     }
     b -= g.H;
@@ -200,11 +210,10 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
 // Stage B blocks are two waves: an H block splits its row's L2 pass into a
 // recompute wave and a backward wave (pair_split_body); a D2 block runs two
 // anti-diagonal L7 chains, one per wave.
-// A banded stage B (d7.band: the diagonal pair's steps [kb, ke)) runs the H
-// rows -- whole-row chains, the launch's critical path -- only with the first
-// band.
+// A banded stage B (d7.band: the diagonal pair's steps [kb, ke)) runs no H
+// rows: the banded schedule's stage A ran them (stage_a_kernel<.., HP>).
 __host__ __device__ inline int stage_b_rows(const PairArgs &d7, const Geom &g) {
-    return d7.band.ke > 0 && d7.band.kb > 0 ? 0 : g.H;
+    return d7.band.ke > 0 ? 0 : g.H;
 }
 
 template <int V, bool FULL>
@@ -221,13 +230,20 @@ __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, 
     if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(d7, g, path, nullptr, nullptr);
 }
 
-hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
-                          hipStream_t st) {
+template <bool HP>
+static void launch_stage_a_t(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6,
+                             const PairArgs &h2, Geom g, hipStream_t st) {
     const dim3 grid(g.H + 2 * g.W);
-    if (g.D == 32) stage_a_kernel<1, false><<<grid, 64, 0, st>>>(h1, l5, d6, g);
-    else if (g.D == 64) stage_a_kernel<1, true><<<grid, 64, 0, st>>>(h1, l5, d6, g);
-    else if (g.D == 128) stage_a_kernel<2, true><<<grid, 64, 0, st>>>(h1, l5, d6, g);
-    else stage_a_kernel<4, true><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    if (g.D == 32) stage_a_kernel<1, false, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    else if (g.D == 64) stage_a_kernel<1, true, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    else if (g.D == 128) stage_a_kernel<2, true, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    else stage_a_kernel<4, true, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+}
+
+hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
+                          hipStream_t st, const PairArgs *h2) {
+    if (h2) launch_stage_a_t<true>(h1, l5, d6, *h2, g, st);
+    else launch_stage_a_t<false>(h1, l5, d6, h1, g, st);
     return hipGetLastError();
 }
 
