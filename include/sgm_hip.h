@@ -230,7 +230,7 @@ typedef struct sgm_kernel_stat {
     char name[32];      /* kernel class, e.g. "sweep_L3_acc" */
     int launches;       /* completed launches since the last read */
     double total_ms;    /* sum of event-measured durations */
-    double elems;       /* pixel-disparity elements touched per launch */
+    double elems;       /* pixel-disparity elements touched per launch (mean over the launches) */
 } sgm_kernel_stat;
 
 /* enable != 0: every subsequent launch is bracketed by two HIP events on the

@@ -73,9 +73,10 @@ struct sgm_handle {
     // profiling (sgm_set_profiling)
     int profiling;
     std::vector<hipEvent_t> ev_pool;
-    struct Pending { int cls; hipEvent_t a, b; };
+    struct Pending { int cls; double elems; hipEvent_t a, b; };
     std::vector<Pending> pending;
     std::vector<sgm_kernel_stat> stats;
+    std::vector<double> stat_elems;  // elements of the class's launches since the last readout
 };
 
 namespace {
@@ -229,6 +230,7 @@ int stat_class(sgm_handle *h, const char *name, double elems) {
     snprintf(st.name, sizeof(st.name), "%s", name);
     st.elems = elems;
     h->stats.push_back(st);
+    h->stat_elems.push_back(0.0);
     return (int)h->stats.size() - 1;
 }
 
@@ -241,7 +243,7 @@ hipError_t timed(sgm_handle *h, const char *name, double elems, hipStream_t st, 
     hipError_t e = hipEventRecord(a, st);
     if (e == hipSuccess) e = fn();
     if (e == hipSuccess) e = hipEventRecord(b, st);
-    h->pending.push_back({stat_class(h, name, elems), a, b});
+    h->pending.push_back({stat_class(h, name, elems), elems, a, b});
     return e;
 }
 
@@ -885,18 +887,22 @@ int sgm_get_profile(sgm_handle *h, sgm_kernel_stat *out, int max, int *count) {
         HIPCHK(h, hipEventElapsedTime(&ms, p.a, p.b));
         h->stats[p.cls].launches += 1;
         h->stats[p.cls].total_ms += ms;
+        h->stat_elems[p.cls] += p.elems;
         h->ev_pool.push_back(p.a);
         h->ev_pool.push_back(p.b);
     }
     h->pending.clear();
     int n = 0;
-    for (auto &st : h->stats) {
+    for (size_t k = 0; k < h->stats.size(); ++k) {
+        sgm_kernel_stat &st = h->stats[k];
         if (st.launches == 0) continue;
+        st.elems = h->stat_elems[k] / st.launches;  // banded launches differ in size
         if (out && n < max) out[n] = st;
         ++n;
     }
     if (count) *count = out ? (n < max ? n : max) : n;
     for (auto &st : h->stats) { st.launches = 0; st.total_ms = 0; }
+    for (auto &e : h->stat_elems) e = 0.0;
     return SGM_OK;
 }
 

@@ -20,6 +20,7 @@ NAMES = [("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
          ("vfwd_kernel", "vfwd"), ("cost_h_kernel", "cost_h"), ("cost_h2_kernel", "cost_h"),
          ("cost_h_global_kernel", "cost_h"),
          ("census_kernel", "census"), ("lr_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc"),
+         ("sweep_split_kernel<7", "sweep_L8_acc"),
          ("median_fill_kernel", "post_median"), ("cc_local_kernel", "post_cc_local"),
          ("cc_merge_kernel", "post_cc_merge"), ("cc_count_kernel", "post_cc_count"),
          ("cc_apply_kernel", "post_cc_apply"), ("pf_prep_kernel", "post_prep"),
