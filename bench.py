@@ -70,6 +70,10 @@ def bytes_per_elem(name: str, D: int) -> float:
         # multi-role launches (sums of their roles)
         "stage_a": (4.0 + ck) + 8.0 + (4.0 + ck),   # L1 fwd | L5 -> T5 | L6 fwd
         "stage_b": (8.0 + ck) + (12.0 + ck),        # L2 bwd -> S12 | L7 bwd -> T
+        # the banded schedule (volumes above the Infinity Cache): stage A also
+        # runs L2 bwd -> S12, stage B's bands only L7 bwd -> T
+        "stage_a_hp": (4.0 + ck) + 8.0 + (4.0 + ck) + (8.0 + ck),
+        "stage_b_d2": 12.0 + ck,
     }
     if name in table:
         return table[name]

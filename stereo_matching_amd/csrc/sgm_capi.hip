@@ -350,7 +350,7 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     // banded: stage A runs the whole H pair (S12), stage B's bands only the
     // diagonal pair
     const bool banded = BR > 0 && !defer_final;
-    HIPCHK(h, timed(h, "stage_a", elems, st, [&] {
+    HIPCHK(h, timed(h, banded ? "stage_a_hp" : "stage_a", elems, st, [&] {
                return sgm::launch_stage_a(h1, l5, d6, h->g, st, banded ? &h2 : nullptr);
            }));
     if (BR == 0 || defer_final)
@@ -371,7 +371,7 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
             const int ke = kb + BR < H ? kb + BR : H;
             const double be = (double)(ke - kb) / H * elems;
             d7.band = {kb, ke, h->d_carry[view][0]};
-            HIPCHK(h, timed(h, "stage_b", be, st,
+            HIPCHK(h, timed(h, "stage_b_d2", be, st,
                             [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
             l8.band = {kb, ke, h->d_carry[view][1]};
             pa.band = {kb, ke, h->d_carry[view][2]};

@@ -210,19 +210,16 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
 // Stage B blocks are two waves: an H block splits its row's L2 pass into a
 // recompute wave and a backward wave (pair_split_body); a D2 block runs two
 // anti-diagonal L7 chains, one per wave.
-// A banded stage B (d7.band: the diagonal pair's steps [kb, ke)) runs no H
-// rows: the banded schedule's stage A ran them (stage_a_kernel<.., HP>).
-__host__ __device__ inline int stage_b_rows(const PairArgs &d7, const Geom &g) {
-    return d7.band.ke > 0 ? 0 : g.H;
-}
-
-template <int V, bool FULL>
+// HROWS = false: a banded stage B (d7.band: the diagonal pair's steps
+// [kb, ke)) without H rows -- the banded schedule's stage A ran them
+// (stage_a_kernel<.., HP>).
+template <int V, bool FULL, bool HROWS>
 __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
     constexpr int K = pair_k<V>();
     __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
     const int b = bid_x(), wave = wave_id();
-    const int nh = stage_b_rows(d7, g);
-    if (b < nh) {
+    const int nh = HROWS ? g.H : 0;
+    if (HROWS && b < nh) {
         pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K, 3>(h2, g, b, wave, lds, nullptr);
         return;
     }
@@ -247,12 +244,18 @@ hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArg
     return hipGetLastError();
 }
 
+template <bool HROWS>
+static void launch_stage_b_t(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st) {
+    const dim3 grid((HROWS ? g.H : 0) + (g.W + 1) / 2);
+    if (g.D == 32) stage_b_kernel<1, false, HROWS><<<grid, 128, 0, st>>>(h2, d7, g);
+    else if (g.D == 64) stage_b_kernel<1, true, HROWS><<<grid, 128, 0, st>>>(h2, d7, g);
+    else if (g.D == 128) stage_b_kernel<2, true, HROWS><<<grid, 128, 0, st>>>(h2, d7, g);
+    else stage_b_kernel<4, true, HROWS><<<grid, 128, 0, st>>>(h2, d7, g);
+}
+
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st) {
-    const dim3 grid(stage_b_rows(d7, g) + (g.W + 1) / 2);
-    if (g.D == 32) stage_b_kernel<1, false><<<grid, 128, 0, st>>>(h2, d7, g);
-    else if (g.D == 64) stage_b_kernel<1, true><<<grid, 128, 0, st>>>(h2, d7, g);
-    else if (g.D == 128) stage_b_kernel<2, true><<<grid, 128, 0, st>>>(h2, d7, g);
-    else stage_b_kernel<4, true><<<grid, 128, 0, st>>>(h2, d7, g);
+    if (d7.band.ke > 0) launch_stage_b_t<false>(h2, d7, g, st);
+    else launch_stage_b_t<true>(h2, d7, g, st);
     return hipGetLastError();
 }
 

@@ -29,6 +29,12 @@ NAMES = [("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
 
 
 def short(name):
+    # the banded schedule's stage kernels (template flag HP / HROWS)
+    for key, flag, val in (("stage_a_kernel<", "true", "stage_a_hp"), ("stage_b_kernel<", "false", "stage_b_d2")):
+        if key in name:
+            args = name[name.index(key) + len(key):].split(">")[0].split(", ")
+            if len(args) == 3 and args[2] == flag:
+                return val
     for key, val in NAMES:
         if key in name:
             return val
