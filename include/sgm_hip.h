@@ -23,8 +23,9 @@
  * volumes, checkpoints, post-filter and LKRefine buffers), so the library
  * orders calls made on different streams: a call whose stream differs from
  * the previous call's first makes its stream wait for the previous call's
- * work (an event recorded at the end of every call).  Calls on one stream
- * are ordered by the stream itself.  Device entry points return after
+ * work (an event it records on the previous call's stream, which must
+ * therefore still exist).  Calls on one stream are ordered by the stream
+ * itself and record nothing.  Device entry points return after
  * enqueueing, EXCEPT with post_filter: its median fill blocks the calling
  * host thread on an event once per two fill launches to read a convergence
  * counter (sgm_post_filter_device, and sgm_process_device with

@@ -48,7 +48,8 @@ __device__ __forceinline__ void stamp_flush(int role, long long t0) {
 }
 #endif
 
-template <int DIR, int V, int MODE, bool FULL, int PF>
+// BAND: a.band's steps only (backward diagonals, DIR 6 / 7)
+template <int DIR, int V, int MODE, bool FULL, int PF, bool BAND = false>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, int path) {
     static_assert(MODE != SWEEP_FINAL, "the final pass is pair_final_kernel");
 #ifdef SGM_STAMPS
@@ -62,8 +63,8 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
     const int e0 = lane * V;
     const bool active = FULL || e0 < g.D;
     constexpr bool NEED_ACC = MODE == SWEEP_ACC;
-    // band: steps [kb, ke) (backward diagonals only; others run whole chains)
-    constexpr bool BANDED = DIR >= 6;
+    static_assert(!BAND || DIR >= 6, "bands of backward diagonal sweeps");
+    constexpr bool BANDED = BAND;
     const int kb = BANDED ? a.band.kb : 0;
     const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
 
@@ -424,7 +425,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
 
 // tb/pb: the FINAL mode's LDS ring (two chunks of K total-cost rows and
 // pixel positions), unused otherwise.
-template <int FAM, int V, bool FULL, int MODE>
+template <int FAM, int V, bool FULL, int MODE, bool BAND = false>
 __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, int path,
                                               float (*tb)[family_k<FAM, V>()][tbuf_stride<V>()],
                                               long long (*pb)[family_k<FAM, V>()]) {
@@ -450,7 +451,8 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
     // band (PAIR_D2 ACC, the frame schedule's stage B): backward steps
     // [kb, ke) = segments s_lo .. s_hi (backward step block c is segment
     // nseg-1-c)
-    constexpr bool BANDED = FAM == PAIR_D2 && MODE == PAIR_ACC;
+    static_assert(!BAND || (FAM == PAIR_D2 && MODE == PAIR_ACC), "bands of the diagonal pair");
+    constexpr bool BANDED = BAND;
     const int kb = BANDED ? a.band.kb : 0;
     const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
     const int s_hi = nseg - 1 - kb / K, s_lo = nseg - (ke + K - 1) / K;
@@ -655,7 +657,8 @@ struct SplitFinalLds {
 // NB: register buffers of segment costs in the producer (NB-1 segments of
 // loads in flight while one is recomputed); RH: the consumer's ring of
 // accumulator loads is RH*K steps deep (chunks processed RH at a time).
-template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1, int NWTA = 1>
+template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1, int NWTA = 1,
+          bool BAND = false>
 __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g, int path,
                                                 int wave, SplitLds<K, V> &L,
                                                 SplitFinalLds<K, V> *F) {
@@ -704,7 +707,8 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
     const long long lin_st = FAM == PAIR_H ? D : WD;
     // band (PAIR_V): backward steps [kb, ke) = chunks [c_lo, c_hi) = segments
     // s_lo .. s_hi (chunk c is segment nseg-1-c)
-    constexpr bool BANDED = FAM == PAIR_V;
+    static_assert(!BAND || FAM == PAIR_V, "bands of the final pass");
+    constexpr bool BANDED = BAND;
     const int kb = BANDED ? a.band.kb : 0;
     const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
     const int c_lo = kb / K, c_hi = (ke + K - 1) / K;

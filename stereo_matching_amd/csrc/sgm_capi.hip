@@ -37,8 +37,8 @@ struct sgm_handle {
     hipStream_t st;       // the handle's own stream (host API, stages)
     hipStream_t aux[1];      // right view (two-view frames)
     hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1, ev_pf;
-    hipEvent_t ev_last;   // end of the last entry point's work (StreamScope)
-    hipStream_t last_st;  // ... and the stream it ran on (null: none yet)
+    hipEvent_t ev_last;   // recorded on last_st when a call comes on another stream (StreamScope)
+    hipStream_t last_st;  // the stream of the last entry point's work (null: none yet)
     uint8_t *d_in[2];     // full-size input staging (host API)
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
@@ -96,19 +96,20 @@ struct DeviceGuard {
 // Every entry point's work shares the handle's scratch (cost volumes,
 // checkpoints, post-filter and LKRefine buffers), whichever stream the caller
 // passes.  A StreamScope orders calls on different streams: if this call's
-// stream differs from the previous call's, it first waits for the event the
-// previous call recorded at its end; on leaving it records that event on its
-// own stream.  Calls on one stream pay only the record.
+// stream differs from the previous call's, it records an event on the
+// previous stream -- behind everything enqueued there so far, the previous
+// call's work included -- and makes its own stream wait for it.  Calls on one
+// stream record nothing (an event record costs the next kernel a ~5 us
+// dispatch gap: the gap between back-to-back frames in the rocprof trace).
 struct StreamScope {
     sgm_handle *h;
     hipStream_t st;
     StreamScope(sgm_handle *handle, void *stream)
         : h(handle), st(stream ? (hipStream_t)stream : handle->st) {
-        if (h->last_st && h->last_st != st) (void)hipStreamWaitEvent(st, h->ev_last, 0);
+        if (h->last_st && h->last_st != st && hipEventRecord(h->ev_last, h->last_st) == hipSuccess)
+            (void)hipStreamWaitEvent(st, h->ev_last, 0);
     }
-    ~StreamScope() {
-        if (hipEventRecord(h->ev_last, st) == hipSuccess) h->last_st = st;
-    }
+    ~StreamScope() { h->last_st = st; }
 };
 
 int set_err(sgm_handle *h, int code, const char *fmt, ...) {

@@ -150,11 +150,12 @@ __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
 template <int V, bool FULL>
 constexpr int final_nwta() { return FULL ? 2 : 1; }
 
-template <int V, bool FULL>
+// BAND: one band of the banded backward phase (a.band)
+template <int V, bool FULL, bool BAND = false>
 __global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
     __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
-    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>()>(
+    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>(), BAND>(
         a, g, bid_x(), wave_id(), lds.s, &lds);
 }
 
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, 
         return;
     }
     const int path = 2 * (b - nh) + wave;
-    if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(d7, g, path, nullptr, nullptr);
+    if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC, !HROWS>(d7, g, path, nullptr, nullptr);
 }
 
 template <bool HP>
@@ -304,12 +305,18 @@ static void launch_bwd_t(const PairArgs &a, Geom g, hipStream_t st) {
     else pair_bwd_kernel<FAM, 4, true, MODE><<<grid, 64, 0, st>>>(a, g);
 }
 
-static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
+template <bool BAND>
+static void launch_final_b(const PairArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(g.W);
-    if (g.D == 32) pair_final_kernel<1, false><<<grid, 64 * (2 + final_nwta<1, false>()), 0, st>>>(a, g);
-    else if (g.D == 64) pair_final_kernel<1, true><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a, g);
-    else if (g.D == 128) pair_final_kernel<2, true><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a, g);
-    else pair_final_kernel<4, true><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a, g);
+    if (g.D == 32) pair_final_kernel<1, false, BAND><<<grid, 64 * (2 + final_nwta<1, false>()), 0, st>>>(a, g);
+    else if (g.D == 64) pair_final_kernel<1, true, BAND><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a, g);
+    else if (g.D == 128) pair_final_kernel<2, true, BAND><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a, g);
+    else pair_final_kernel<4, true, BAND><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a, g);
+}
+
+static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
+    if (a.band.ke > 0) launch_final_b<true>(a, g, st);
+    else launch_final_b<false>(a, g, st);
 }
 
 hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStream_t st) {

@@ -22,9 +22,9 @@
 
 namespace sgm {
 
-template <int DIR, int V, int MODE, bool FULL, int PF>
+template <int DIR, int V, int MODE, bool FULL, int PF, bool BAND = false>
 __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
-    sweep_body<DIR, V, MODE, FULL, PF>(a, g, bid_x());
+    sweep_body<DIR, V, MODE, FULL, PF, BAND>(a, g, bid_x());
 }
 
 // Diagonal INIT/ACC sweeps (the L8 pass): memory wave + DP wave
@@ -54,7 +54,7 @@ template <int DIR, int MODE>
 static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(DIR < 2 ? g.H : g.W);
     if constexpr (DIR >= 4 && MODE != SWEEP_STORE_L) {
-        if (a.band.ke == 0 && use_split_sweep(g)) {  // (banded sweeps: the one-wave body)
+        if (a.band.ke == 0 && use_split_sweep(g)) {  // (bands: the one-wave body, below)
             if (g.D == 32)
                 sweep_split_kernel<DIR, 1, MODE, false><<<grid, 128, 0, st>>>(a, g);
             else if (g.D == 64)
@@ -67,6 +67,19 @@ static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
         }
     }
     constexpr int PF = sweep_pf<DIR>();
+    if constexpr (DIR >= 6 && MODE == SWEEP_ACC) {
+        if (a.band.ke > 0) {  // one band of the banded backward phase
+            if (g.D == 32)
+                sweep_kernel<DIR, 1, MODE, false, PF, true><<<grid, 64, 0, st>>>(a, g);
+            else if (g.D == 64)
+                sweep_kernel<DIR, 1, MODE, true, PF, true><<<grid, 64, 0, st>>>(a, g);
+            else if (g.D == 128)
+                sweep_kernel<DIR, 2, MODE, true, PF, true><<<grid, 64, 0, st>>>(a, g);
+            else
+                sweep_kernel<DIR, 4, MODE, true, PF / 2, true><<<grid, 64, 0, st>>>(a, g);
+            return;
+        }
+    }
     if (g.D == 32)
         sweep_kernel<DIR, 1, MODE, false, PF><<<grid, 64, 0, st>>>(a, g);
     else if (g.D == 64)
