@@ -74,6 +74,10 @@ def bytes_per_elem(name: str, D: int) -> float:
         # runs L2 bwd -> S12, stage B's bands only L7 bwd -> T
         "stage_a_hp": (4.0 + ck) + 8.0 + (4.0 + ck) + (8.0 + ck),
         "stage_b_d2": 12.0 + ck,
+        # the forward bands: stage A's diagonal roles per band (L5 -> T5 |
+        # L6 fwd), then the whole H pair as its own launch
+        "stage_a_d": 8.0 + (4.0 + ck),
+        "stage_a_h": (4.0 + ck) + (8.0 + ck),
     }
     if name in table:
         return table[name]

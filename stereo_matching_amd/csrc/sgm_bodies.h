@@ -48,7 +48,8 @@ __device__ __forceinline__ void stamp_flush(int role, long long t0) {
 }
 #endif
 
-// BAND: a.band's steps only (backward diagonals, DIR 6 / 7)
+// BAND: a.band's steps only (the backward diagonals DIR 6 / 7 of the
+// backward bands, L5 (DIR 4) of the forward bands)
 template <int DIR, int V, int MODE, bool FULL, int PF, bool BAND = false>
 __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, int path) {
     static_assert(MODE != SWEEP_FINAL, "the final pass is pair_final_kernel");
@@ -63,7 +64,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs &a, const Geom &g, in
     const int e0 = lane * V;
     const bool active = FULL || e0 < g.D;
     constexpr bool NEED_ACC = MODE == SWEEP_ACC;
-    static_assert(!BAND || DIR >= 6, "bands of backward diagonal sweeps");
+    static_assert(!BAND || DIR >= 4, "bands of diagonal sweeps");
     constexpr bool BANDED = BAND;
     const int kb = BANDED ? a.band.kb : 0;
     const int ke = BANDED && a.band.ke > 0 ? a.band.ke : n;
@@ -324,7 +325,10 @@ __device__ __forceinline__ void sweep_split_body(const SweepArgs &a, const Geom 
 // Forward direction FD (0 = L1, 2 = L3, 5 = L6) over one chain: the DP of
 // SGM.cpp:93-117 with the cost stream prefetched PF steps ahead; the only
 // output is the checkpoint set.
-template <int FD, int V, bool FULL, int PF>
+// BAND (FD 5, the forward bands above the Infinity Cache): steps [kb, ke)
+// of the chain, whole segments (kb, ke = r0 mod K, or ke = n), the state
+// entering the band from a.band.carry and the state leaving it stored there.
+template <int FD, int V, bool FULL, int PF, bool BAND = false>
 __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, int path) {
 #ifdef SGM_STAMPS
     const long long st_t0 = __builtin_amdgcn_s_memtime();
@@ -352,10 +356,20 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     // then yields L = C, the reference's path start (SGM.cpp:93-98).  Block
     // nseg-1 stores into the unused last slot.
     const int vs = K - r0;
+    static_assert(!BAND || FD == 5, "bands of the forward diagonal");
+    const int kb = BAND ? a.band.kb : 0;
+    const int ke = BAND && a.band.ke > 0 ? a.band.ke : n;
+    // the first position walked: the virtual start, or the band's first step
+    const int s0 = kb > 0 ? kb : -vs;
     Cursor<FD> cc, pc;
-    cc.init(path, H, W, g.D);
-    pc.init(path, H, W, g.D);
-    int ppos = -vs;  // position of the next ring refill
+    if (BAND && kb > 0) {
+        cc.init_at(path, kb, H, W, g.D);
+        pc.init_at(path, kb, H, W, g.D);
+    } else {
+        cc.init(path, H, W, g.D);
+        pc.init(path, H, W, g.D);
+    }
+    int ppos = s0;  // position of the next ring refill
     // rows (FD 0): a plain running pointer; positions past the row's end read
     // the next row or the volume guard (kVolGuard) and are never consumed
     const float *hrow = a.cost + (size_t)path * W * g.D;
@@ -384,10 +398,15 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
         }
     };
     float prev[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) prev[v] = 0.0f;
     float pmin = 0.0f;
-    int cpos = -vs;  // position of the next step
+    if (BAND && kb > 0) {  // the chain state entering the band
+        load_v<V>(prev, a.band.carry + (size_t)path * g.D + e0, active);
+        pmin = wave_min(lane_min(prev));
+    } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = 0.0f;
+    }
+    int cpos = s0;  // position of the next step
 
     auto step = [&](int u, bool refill) {
         float L[V];
@@ -407,7 +426,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
         ++cpos;
         if (refill) refetch(cb[u]);
     };
-    const int total = nseg * K;
+    const int total = ke - s0;  // nseg * K for the whole chain
     int k0 = 0;
     for (; k0 + PF <= total; k0 += PF) {
 #pragma unroll
@@ -416,6 +435,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
 #pragma unroll
     for (int u = 0; u < PF; ++u)
         if (k0 + u < total) step(u, false);
+    if (BAND && ke < n) store_v<V>(a.band.carry + (size_t)path * g.D + e0, prev, active);
 #ifdef SGM_STAMPS
     stamp_flush(FD == 0 ? 5 : (FD == 5 ? 6 : 7), st_t0);
 #endif

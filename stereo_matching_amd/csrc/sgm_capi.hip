@@ -54,6 +54,7 @@ struct sgm_handle {
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
     float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
     int band_rows;        // rows per band of the backward phase (0: whole volume)
+    bool fwd_bands;       // frames also run vfwd and stage A's diagonal roles in bands
     // post_filter scratch (sgm_post.hip)
     float *d_pf_orig;     // the map as it entered the median fill
     float *d_pf_work;     // contiguous working map (pitched callers)
@@ -327,8 +328,18 @@ int band_rows_for(Geom g) {
 //   final:   L4 bwd recomputing L3: total = ((S12 + L3) + L4) + T -> WTA
 // (the reference's order, SGM.cpp:386-390).  T may alias the dead
 // horizontally filtered volume.
+// fwd_bands (banded frames): the view's vertical filter + L3 forward pass
+// (vfwd, from the horizontally filtered volume T) and stage A's diagonal
+// roles run in forward bands first, top band first, so that each band's
+// final cost stays in the Infinity Cache from vfwd to L5 and L6; the whole H
+// pair follows as its own launch (DESIGN.md "Bands").
+// part AGG_FWD stops after the forward bands and leaves the H pair's
+// arguments in hp[0..1] (the caller launches both views' H pairs at once);
+// AGG_BWD then runs the rest.
+enum AggPart { AGG_ALL = 0, AGG_FWD = 1, AGG_BWD = 2 };
 int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *T, uint16_t *disp,
-                   float *sub, hipStream_t st, bool need_v_ckpt, sgm::PairArgs *defer_final = nullptr) {
+                   float *sub, hipStream_t st, bool need_v_ckpt, sgm::PairArgs *defer_final = nullptr,
+                   bool fwd_bands = false, int part = AGG_ALL, sgm::PairArgs *hp = nullptr) {
     float **ck = h->d_ck[view];
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     sgm::PairArgs pa = pair_args(h);
@@ -351,9 +362,38 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     // banded: stage A runs the whole H pair (S12), stage B's bands only the
     // diagonal pair
     const bool banded = BR > 0 && !defer_final;
-    HIPCHK(h, timed(h, banded ? "stage_a_hp" : "stage_a", elems, st, [&] {
-               return sgm::launch_stage_a(h1, l5, d6, h->g, st, banded ? &h2 : nullptr);
-           }));
+    if (part == AGG_BWD) {
+        // stage A ran (AGG_FWD + the caller's H pair launch)
+    } else if (banded && fwd_bands) {
+        sgm::PairArgs va = pair_args(h);
+        va.ckpt = ck[sgm::PAIR_V];
+        // band edges at H - m*BR (multiples of 16 rows from the bottom, as
+        // the backward bands): whole segments of every family
+        const int nb = (H + BR - 1) / BR;
+        for (int m = nb - 1; m >= 0; --m) {
+            const int rb = H - (m + 1) * BR > 0 ? H - (m + 1) * BR : 0, re = H - m * BR;
+            const double be = (double)(re - rb) / H * elems;
+            va.band = {rb, re, h->d_carry[view][2]};
+            HIPCHK(h, timed(h, "vfwd", be, st, [&] {
+                       return sgm::launch_vfwd(h->d_ch[view], h->d_c[view], va, h->g, st);
+                   }));
+            l5.band = {rb, re, h->d_carry[view][0]};
+            d6.band = {rb, re, h->d_carry[view][1]};
+            HIPCHK(h, timed(h, "stage_a_d", be, st,
+                            [&] { return sgm::launch_stage_a_band(l5, d6, h->g, st); }));
+        }
+        if (part == AGG_FWD) {
+            hp[0] = h1;
+            hp[1] = h2;
+            return SGM_OK;
+        }
+        HIPCHK(h, timed(h, "stage_a_h", elems, st,
+                        [&] { return sgm::launch_stage_a_hpair(&h1, &h2, 1, h->g, st); }));
+    } else {
+        HIPCHK(h, timed(h, banded ? "stage_a_hp" : "stage_a", elems, st, [&] {
+                   return sgm::launch_stage_a(h1, l5, d6, h->g, st, banded ? &h2 : nullptr);
+               }));
+    }
     if (BR == 0 || defer_final)
         HIPCHK(h, timed(h, "stage_b", elems, st,
                         [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
@@ -397,13 +437,14 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
 // the vertical IIR fused with the L3 forward pass (vfwd), into view slot
 // `view`'s buffers.
 int vfwd_view(sgm_handle *h, int view, hipStream_t st);
-int cost_view(sgm_handle *h, int view, int dsi, const uint8_t *sky, int sky_pitch, hipStream_t st) {
+int cost_view(sgm_handle *h, int view, int dsi, const uint8_t *sky, int sky_pitch, hipStream_t st,
+              bool vfwd = true) {
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     HIPCHK(h, timed(h, "cost_h", elems, st, [&] {
                return sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky, sky_pitch, dsi, 1, h->g,
                                          h->d_ch[view], st);
            }));
-    return vfwd_view(h, view, st);
+    return vfwd ? vfwd_view(h, view, st) : SGM_OK;
 }
 
 int vfwd_view(sgm_handle *h, int view, hipStream_t st) {
@@ -491,20 +532,24 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     const bool both_h = h->nviews == 2 && aux1 == st && (d_sky_l == nullptr) == (d_sky_r == nullptr) &&
                         sgm::cost_h2_supported(g, d_sky_l != nullptr);
     if (h->nviews == 2 && !both_h && aux1 != st) HIPCHK(h, hipEventRecord(h->ev_ct, st));
+    // banded frames run vfwd in forward bands inside aggregate_view
+    const bool fwd_bands = h->fwd_bands;
     if (both_h) {
         HIPCHK(h, timed(h, "cost_h", 2.0 * npx * g.D, st, [&] {
                    return sgm::launch_cost_h2(h->d_ct[0], h->d_ct[1], d_sky_l, d_sky_r, sky_pitch, g,
                                               h->d_ch[0], h->d_ch[1], st);
                }));
-        if ((rc = vfwd_view(h, 1, st)) != SGM_OK) return rc;
-        if ((rc = vfwd_view(h, 0, st)) != SGM_OK) return rc;
+        if (!fwd_bands) {
+            if ((rc = vfwd_view(h, 1, st)) != SGM_OK) return rc;
+            if ((rc = vfwd_view(h, 0, st)) != SGM_OK) return rc;
+        }
     } else {
         if (h->nviews == 2) {
             if (aux1 != st) HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
-            if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1)) != SGM_OK) return rc;
+            if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1, !fwd_bands)) != SGM_OK) return rc;
         }
         if ((rc = cost_view(h, 0, right_only ? 1 : 0, right_only ? d_sky_r : d_sky_l, sky_pitch,
-                            st)) != SGM_OK)
+                            st, !fwd_bands)) != SGM_OK)
             return rc;
     }
     // Volumes larger than the 256 MB Infinity Cache gain nothing from
@@ -517,13 +562,29 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // one view with a dense output map: the final pass writes the sub-pixel
     // map straight into it (no device copy after the frame)
     const bool direct_out = h->nviews == 1 && out_pitch == g.W;
-    if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0],
-                             direct_out ? d_out : h->d_sub[0], st, false,
-                             both_final ? &fin[0] : nullptr)) != SGM_OK)
+    // banded frames with two views on one stream: both views' forward bands,
+    // then both H pairs in one launch, then each view's backward bands
+    const bool split_h = fwd_bands && h->nviews == 2 && aux1 == st;
+    float *sub0 = direct_out ? d_out : h->d_sub[0];
+    if (split_h) {
+        sgm::PairArgs hp[2][2];
+        for (int v = 0; v < 2; ++v)
+            if ((rc = aggregate_view(h, v, h->d_c[v], h->d_s[v], h->d_ch[v], h->d_disp[v],
+                                     v ? h->d_sub[1] : sub0, st, false, nullptr, true, AGG_FWD,
+                                     hp[v])) != SGM_OK)
+                return rc;
+        const sgm::PairArgs h1[2] = {hp[0][0], hp[1][0]}, h2[2] = {hp[0][1], hp[1][1]};
+        HIPCHK(h, timed(h, "stage_a_h", 2.0 * npx * g.D, st,
+                        [&] { return sgm::launch_stage_a_hpair(h1, h2, 2, g, st); }));
+    }
+    const int part = split_h ? AGG_BWD : AGG_ALL;
+    if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], sub0, st, false,
+                             both_final ? &fin[0] : nullptr, fwd_bands, part)) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
         if ((rc = aggregate_view(h, 1, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
-                                 aux1, false, both_final ? &fin[1] : nullptr)) != SGM_OK)
+                                 aux1, false, both_final ? &fin[1] : nullptr, fwd_bands,
+                                 part)) != SGM_OK)
             return rc;
         if (both_final)
             HIPCHK(h, timed(h, "pair_bwd_L4_final", 2.0 * npx * g.D, st,
@@ -750,10 +811,15 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if ((rc = dalloc(h, &h->d_sub[v], npx))) break;
             for (int f = 0; f < 3 && !rc; ++f)
                 rc = dalloc(h, &h->d_ck[v][f], sgm::pair_ckpt_floats(f, h->g));
+            // slot 2 also holds vfwd's forward-band state (3 D-vectors per column)
             for (int f = 0; f < 3 && !rc; ++f)
-                rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D);
+                rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D * (f == 2 ? 3 : 1));
         }
         h->band_rows = band_rows_for(h->g);
+        {
+            const char *e = getenv("SGM_FWD_BANDS");
+            h->fwd_bands = h->band_rows > 0 && !(e && *e == '0');
+        }
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {
                 if ((rc = dalloc(h, &h->d_disp[v], npx))) break;

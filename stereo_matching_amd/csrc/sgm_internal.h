@@ -38,6 +38,8 @@ enum SweepMode {
 // whole chain.  The backward phase (stage B's diagonal pair, L8, final) runs
 // band by band above the Infinity Cache, so that a band's cost volume and T
 // stay cached from one pass to the next (DESIGN.md "Bands").
+// Forward passes run bands too (rows [kb, ke) walked down, top band first:
+// vfwd, L5, L6), with the same edges.
 struct Band {
     int kb, ke;
     float *carry;
@@ -99,6 +101,12 @@ hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStre
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
                           hipStream_t st, const PairArgs *h2 = nullptr);
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st);
+// the forward bands (DESIGN.md "Bands"): the whole H pair (L1 fwd, then L2
+// bwd -> h2[v].out) of nviews views as one launch, and one band (l5.band, d6.band)
+// of stage A's diagonal roles (L5 -> T5, L6 fwd)
+hipError_t launch_stage_a_hpair(const PairArgs *h1, const PairArgs *h2, int nviews, Geom g,
+                                hipStream_t st);
+hipError_t launch_stage_a_band(const SweepArgs &l5, const PairArgs &d6, Geom g, hipStream_t st);
 hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st);
 
 // bm_rows: BM.cpp:24-25 decimation (rows not strided by the scale); src2/ct2:

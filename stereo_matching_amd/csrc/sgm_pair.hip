@@ -39,7 +39,11 @@ size_t pair_ckpt_floats(int family, Geom g) {
 // and fed straight into the L3 DP; L3 is checkpointed for the PAIR_V
 // backward kernel.  The raw rows the IIR adds (raw[i + WIN/2 + 1]) stream
 // through a register ring PF rows ahead.
-template <int V, bool FULL, int WIN, int PF>
+// BAND (the forward bands above the Infinity Cache): rows [a.band.kb,
+// a.band.ke) only, the filter's running sum, its last output and the L3 state
+// entering the band read from a.band.carry (3 D-vectors per column) and the
+// state leaving it written back there.
+template <int V, bool FULL, int WIN, int PF, bool BAND = false>
 __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
                                                   float *__restrict__ out, PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
@@ -56,34 +60,45 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     const int nseg = (H + K - 1) / K;
     const int r0 = H - (nseg - 1) * K;
     float *ck = a.ckpt + (size_t)j * nseg * g.D + e0;
-    int next_ck = r0 - 1, ck_i = 0;
+    const int rb = BAND ? a.band.kb : 0;
+    const int re = BAND && a.band.ke > 0 ? a.band.ke : H;
+    // checkpoints sit after rows r0-1 + mK; the first one at or after rb
+    int ck_i = rb <= r0 - 1 ? 0 : (rb - r0 + K) / K;
+    int next_ck = r0 - 1 + ck_i * K;
     const int T = H - 2 * HALF;
+    float *cy = BAND ? a.band.carry + (size_t)j * 3 * g.D + e0 : nullptr;
 
     float raw0[V], rawl[V], sum[V], o1[V];
     load_v_nt<V>(raw0, col, active);
     load_v_nt<V>(rawl, col + (size_t)(H - 1) * stride, active);  // the only row below LAG+T (WIN=3)
+    float prev[V];
+    float pmin = 0.0f;
+    if (BAND && rb > 0) {  // the filter and path state entering the band
+        load_v<V>(sum, cy, active);
+        load_v<V>(o1, cy + g.D, active);
+        load_v<V>(prev, cy + 2 * g.D, active);
+        pmin = wave_min(lane_min(prev));
+    } else {
 #pragma unroll
-    for (int v = 0; v < V; ++v) sum[v] = 0.0f;
+        for (int v = 0; v < V; ++v) sum[v] = 0.0f;
 #pragma unroll
-    for (int k = 0; k < WIN; ++k) {
-        float r[V];
-        load_v_nt<V>(r, col + (size_t)k * stride, active);
+        for (int k = 0; k < WIN; ++k) {
+            float r[V];
+            load_v_nt<V>(r, col + (size_t)k * stride, active);
 #pragma unroll
-        for (int v = 0; v < V; ++v) sum[v] += r[v];
+            for (int v = 0; v < V; ++v) sum[v] += r[v];
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) o1[v] = 0.0f;
+        // L = 0, minL = 0 before row 0 makes the first step yield L = C (the
+        // path start, SGM.cpp:161-170) without a per-row select (P1, P2 >= 0)
+#pragma unroll
+        for (int v = 0; v < V; ++v) prev[v] = 0.0f;
     }
-#pragma unroll
-    for (int v = 0; v < V; ++v) o1[v] = 0.0f;
     float ring[PF][V];
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        load_v_nt<V>(ring[u], col + (size_t)min(LA + u, H - 1) * stride, active);
-
-    // L = 0, minL = 0 before row 0 makes the first step yield L = C (the
-    // path start, SGM.cpp:161-170) without a per-row select (P1, P2 >= 0)
-    float prev[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) prev[v] = 0.0f;
-    float pmin = 0.0f;
+        load_v_nt<V>(ring[u], col + (size_t)min(rb + LA + u, H - 1) * stride, active);
 
     auto row = [&](int i, int u, bool refill) {
         float c[V];
@@ -122,14 +137,19 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
         pmin = nmin;
         if (refill) load_v_nt<V>(ring[u], col + (size_t)min(i + LA + PF, H - 1) * stride, active);
     };
-    int i0 = 0;
-    for (; i0 + PF <= H; i0 += PF) {
+    int i0 = rb;
+    for (; i0 + PF <= re; i0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) row(i0 + u, u, true);
     }
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        if (i0 + u < H) row(i0 + u, u, false);
+        if (i0 + u < re) row(i0 + u, u, false);
+    if (BAND && re < H) {  // the state leaving the band
+        store_v<V>(cy, sum, active);
+        store_v<V>(cy + g.D, o1, active);
+        store_v<V>(cy + 2 * g.D, prev, active);
+    }
 }
 
 template <int FD, int V, bool FULL, int PF>
@@ -185,11 +205,20 @@ __global__ __launch_bounds__(256) void pair_final2_kernel(PairArgs a0, PairArgs 
 // whole-row chains.  (Two-wave blocks running the backward half split over
 // both waves, as stage B does, were slower: the split's LDS ring on every
 // block of the launch cuts the diagonal roles' occupancy.)
-template <int V, bool FULL, bool HP>
+// ROLES 1 (the forward bands): the diagonal roles only, steps [kb, ke) of each
+// chain (l5.band, d6.band); the H pair then runs as its own launch (grid H,
+// HP) after the last forward band -- its whole-row chains would set every
+// band launch's length.
+template <int V, bool FULL, bool HP, int ROLES = 0>
 __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, PairArgs d6,
                                                      PairArgs h2, Geom g) {
     constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
     int b = bid_x();
+    if constexpr (ROLES == 1) {
+        if (b < g.W) sweep_body<4, V, SWEEP_INIT, FULL, PFD, true>(l5, g, b);
+        else pair_fwd_body<5, V, FULL, PFD, true>(d6, g, b - g.W);
+        return;
+    }
     if (b < g.H) {
         // the H chains (few, long) are the launch's critical path
         __builtin_amdgcn_s_setprio(3);
@@ -206,6 +235,24 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
         return;
     }
     pair_fwd_body<5, V, FULL, PFD>(d6, g, b - g.W);
+}
+
+// The forward bands' H pair (L1 forward, then L2 backward recomputing L1 ->
+// S12, as stage_a_kernel<.., HP>'s H blocks) of one or two views in one
+// launch (workgroup y = view).  With the diagonal roles in the band launches
+// this launch holds only H (per view) single-wave chains, about one per SIMD
+// at HD256, so it waits on memory latency; both views' rows side by side
+// double the loads in flight.
+template <int V, bool FULL>
+__global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, PairArgs h1b,
+                                                   PairArgs h2b, Geom g) {
+    constexpr int PFH = V >= 4 ? 16 : 32;
+    const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
+    const PairArgs &h1 = vb ? h1b : h1a;
+    const PairArgs &h2 = vb ? h2b : h2a;
+    pair_fwd_body<0, V, FULL, PFH>(h1, g, bid_x());
+    __threadfence();  // this wave's checkpoint stores, before it reads them back
+    pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, bid_x(), nullptr, nullptr);
 }
 
 // Stage B blocks are two waves: an H block splits its row's L2 pass into a
@@ -228,20 +275,36 @@ __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, 
     if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC, !HROWS>(d7, g, path, nullptr, nullptr);
 }
 
-template <bool HP>
+template <bool HP, int ROLES = 0>
 static void launch_stage_a_t(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6,
-                             const PairArgs &h2, Geom g, hipStream_t st) {
-    const dim3 grid(g.H + 2 * g.W);
-    if (g.D == 32) stage_a_kernel<1, false, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
-    else if (g.D == 64) stage_a_kernel<1, true, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
-    else if (g.D == 128) stage_a_kernel<2, true, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
-    else stage_a_kernel<4, true, HP><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+                             const PairArgs &h2, Geom g, hipStream_t st, int nblk) {
+    const dim3 grid(nblk);
+    if (g.D == 32) stage_a_kernel<1, false, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    else if (g.D == 64) stage_a_kernel<1, true, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    else if (g.D == 128) stage_a_kernel<2, true, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    else stage_a_kernel<4, true, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
 }
 
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
                           hipStream_t st, const PairArgs *h2) {
-    if (h2) launch_stage_a_t<true>(h1, l5, d6, *h2, g, st);
-    else launch_stage_a_t<false>(h1, l5, d6, h1, g, st);
+    if (h2) launch_stage_a_t<true>(h1, l5, d6, *h2, g, st, g.H + 2 * g.W);
+    else launch_stage_a_t<false>(h1, l5, d6, h1, g, st, g.H + 2 * g.W);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage_a_hpair(const PairArgs *h1, const PairArgs *h2, int nviews, Geom g,
+                                hipStream_t st) {
+    const dim3 grid(g.H, nviews);
+    const PairArgs &b1 = h1[nviews - 1], &b2 = h2[nviews - 1];
+    if (g.D == 32) hpair_kernel<1, false><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);
+    else if (g.D == 64) hpair_kernel<1, true><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);
+    else if (g.D == 128) hpair_kernel<2, true><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);
+    else hpair_kernel<4, true><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage_a_band(const SweepArgs &l5, const PairArgs &d6, Geom g, hipStream_t st) {
+    launch_stage_a_t<false, 1>(d6, l5, d6, d6, g, st, 2 * g.W);
     return hipGetLastError();
 }
 
@@ -281,18 +344,19 @@ hipError_t launch_pair_fwd(int family, const PairArgs &a, Geom g, hipStream_t st
     return hipGetLastError();
 }
 
-template <int WIN>
+template <int WIN, bool BAND>
 static void launch_vfwd_t(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(g.W);
-    if (g.D == 32) vfwd_kernel<1, false, WIN, 16><<<grid, 64, 0, st>>>(in, out, a, g);
-    else if (g.D == 64) vfwd_kernel<1, true, WIN, 16><<<grid, 64, 0, st>>>(in, out, a, g);
-    else if (g.D == 128) vfwd_kernel<2, true, WIN, 16><<<grid, 64, 0, st>>>(in, out, a, g);
-    else vfwd_kernel<4, true, WIN, 8><<<grid, 64, 0, st>>>(in, out, a, g);
+    if (g.D == 32) vfwd_kernel<1, false, WIN, 16, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
+    else if (g.D == 64) vfwd_kernel<1, true, WIN, 16, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
+    else if (g.D == 128) vfwd_kernel<2, true, WIN, 16, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
+    else vfwd_kernel<4, true, WIN, 8, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
 }
 
 hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st) {
-    if (g.scale == 1) launch_vfwd_t<3>(in, out, a, g, st);
-    else launch_vfwd_t<1>(in, out, a, g, st);
+    const bool band = a.band.ke > 0;
+    if (g.scale == 1) band ? launch_vfwd_t<3, true>(in, out, a, g, st) : launch_vfwd_t<3, false>(in, out, a, g, st);
+    else band ? launch_vfwd_t<1, true>(in, out, a, g, st) : launch_vfwd_t<1, false>(in, out, a, g, st);
     return hipGetLastError();
 }
 

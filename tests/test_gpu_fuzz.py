@@ -6,8 +6,8 @@ SGM parameters the C-ABI exposes beyond the reference's constants -- P1, P2
 the LR threshold (inc/Solver.h:16: 1).  The oracle (oracle/sgm_oracle.c)
 takes the same parameters.  Every case runs with both bodies of the diagonal
 L8 sweep (SGM_SWEEP_SPLIT: the one-wave sweep and the memory-wave + DP-wave
-split, which the library picks by volume size), and once more with the
-backward phase in bands (SGM_BAND_ROWS)."""
+split, which the library picks by volume size), and once more in bands
+(SGM_BAND_ROWS; with and without the forward bands, SGM_FWD_BANDS)."""
 from __future__ import annotations
 
 import numpy as np
@@ -50,11 +50,15 @@ def test_random_frame(c, split, monkeypatch):
 
 
 @pytest.mark.parametrize("c", CASES, ids=[f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_V{c['views']}" for c in CASES])
-def test_random_frame_banded(c, monkeypatch):
-    """The backward phase in 16-row bands (the schedule of volumes above the
-    Infinity Cache: stage B's diagonal pair, L8 and the final pass band by
-    band, chain states carried across band edges)."""
+@pytest.mark.parametrize("fwd", ["1", "0"], ids=["fwdbands", "bwdbands"])
+def test_random_frame_banded(c, fwd, monkeypatch):
+    """16-row bands (the schedule of volumes above the Infinity Cache): the
+    forward phase (vfwd, L5, L6) band by band top down, both views' H pairs
+    in one launch, then the backward phase (stage B's diagonal pair, L8 and
+    the final pass) band by band bottom up, chain and filter states carried
+    across band edges; SGM_FWD_BANDS=0 keeps the forward phase whole."""
     monkeypatch.setenv("SGM_BAND_ROWS", "16")
+    monkeypatch.setenv("SGM_FWD_BANDS", fwd)
     _check(c)
 
 

@@ -15,7 +15,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # kernel symbol -> name used by the library's in-process profiler (bench.py)
-NAMES = [("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
+NAMES = [("hpair_kernel", "stage_a_h"), ("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
          ("pair_final_kernel", "pair_bwd_L4_final"), ("pair_final2_kernel", "pair_bwd_L4_final"),
          ("vfwd_kernel", "vfwd"), ("cost_h_kernel", "cost_h"), ("cost_h2_kernel", "cost_h"),
          ("cost_h_global_kernel", "cost_h"),
@@ -29,6 +29,14 @@ NAMES = [("stage_a_kernel", "stage_a"), ("stage_b_kernel", "stage_b"),
 
 
 def short(name):
+    # the forward bands' diagonal stage A launches (template ROLES 1)
+    key = "stage_a_kernel<"
+    if key in name:
+        args = name[name.index(key) + len(key):].split(">")[0].split(", ")
+        if len(args) == 4 and args[3] == "1":
+            return "stage_a_d"
+        if len(args) == 4 and args[2] == "true":
+            return "stage_a_hp"
     # the banded schedule's stage kernels (template flag HP / HROWS)
     for key, flag, val in (("stage_a_kernel<", "true", "stage_a_hp"), ("stage_b_kernel<", "false", "stage_b_d2")):
         if key in name:
