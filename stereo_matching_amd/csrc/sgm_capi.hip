@@ -55,6 +55,7 @@ struct sgm_handle {
     float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
     int band_rows;        // rows per band of the backward phase (0: whole volume)
     bool fwd_bands;       // frames also run vfwd and stage A's diagonal roles in bands
+    int fwd_band_rows;    // rows per forward band (a multiple of 16)
     // post_filter scratch (sgm_post.hip)
     float *d_pf_orig;     // the map as it entered the median fill
     float *d_pf_work;     // contiguous working map (pitched callers)
@@ -369,9 +370,10 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
         va.ckpt = ck[sgm::PAIR_V];
         // band edges at H - m*BR (multiples of 16 rows from the bottom, as
         // the backward bands): whole segments of every family
-        const int nb = (H + BR - 1) / BR;
+        const int FR = h->fwd_band_rows;
+        const int nb = (H + FR - 1) / FR;
         for (int m = nb - 1; m >= 0; --m) {
-            const int rb = H - (m + 1) * BR > 0 ? H - (m + 1) * BR : 0, re = H - m * BR;
+            const int rb = H - (m + 1) * FR > 0 ? H - (m + 1) * FR : 0, re = H - m * FR;
             const double be = (double)(re - rb) / H * elems;
             va.band = {rb, re, h->d_carry[view][2]};
             HIPCHK(h, timed(h, "vfwd", be, st, [&] {
@@ -819,6 +821,10 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         {
             const char *e = getenv("SGM_FWD_BANDS");
             h->fwd_bands = h->band_rows > 0 && !(e && *e == '0');
+            // forward bands may differ in size (SGM_FWD_BAND_ROWS, multiples of 16)
+            const char *f = getenv("SGM_FWD_BAND_ROWS");
+            const int fr = f && *f ? atoi(f) / 16 * 16 : 0;
+            h->fwd_band_rows = fr > 0 ? fr : h->band_rows;
         }
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {

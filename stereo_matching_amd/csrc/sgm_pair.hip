@@ -246,7 +246,11 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
 template <int V, bool FULL>
 __global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, PairArgs h1b,
                                                    PairArgs h2b, Geom g) {
+#ifdef SGM_HPF
+    constexpr int PFH = V >= 4 ? SGM_HPF : 2 * SGM_HPF;
+#else
     constexpr int PFH = V >= 4 ? 16 : 32;
+#endif
     const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
     const PairArgs &h1 = vb ? h1b : h1a;
     const PairArgs &h2 = vb ? h2b : h2a;
