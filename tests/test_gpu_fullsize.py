@@ -5,7 +5,8 @@ compared bit-for-bit with the oracle (it finishes in seconds to tens of
 seconds with OpenMP).  4K256 (config 5's frame) is too large for the oracle
 within the test budget; there the checks are size-independent properties:
 determinism, agreement of the LR-checked map with the two single-view maps,
-and recovery of the synthetic pair's known disparity field.
+recovery of the synthetic pair's known disparity field, and bit-for-bit
+agreement of the banded schedules with the whole-volume one.
 """
 from __future__ import annotations
 
@@ -64,6 +65,28 @@ def test_4k256_properties():
     est = raw1[rows][:, D + 8: w - 8].astype(np.int64)
     hit = np.mean(np.abs(est - g[rows][:, None]) <= 1)
     assert hit > 0.9, hit
+
+
+def test_4k256_schedules_agree(monkeypatch):
+    """config 5's frame through the three schedules of a volume above the
+    Infinity Cache -- forward and backward bands (the default), backward bands
+    only (SGM_FWD_BANDS=0), whole-volume passes (SGM_BAND_ROWS=0, the schedule
+    the oracle pins at K128) -- bit for bit."""
+    h, w, D = 2160, 3840, 256
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=2)
+    sky = synthetic.sky_mask(h, w)
+    maps = []
+    for env in ({}, {"SGM_FWD_BANDS": "0"}, {"SGM_BAND_ROWS": "0"}):
+        for k in ("SGM_FWD_BANDS", "SGM_BAND_ROWS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with SGM(h, w, 1, D, views=2) as sgm:
+            sgm.process(left, right, sky, sky)
+            maps.append((sgm.get_lr_disp().copy(), sgm.get_raw_disp().copy()))
+    for lr, raw in maps[1:]:
+        assert np.array_equal(raw, maps[0][1])
+        assert np.array_equal(_bits(lr), _bits(maps[0][0]))
 
 
 def test_k128_full_pipeline_vs_oracle():
