@@ -188,7 +188,7 @@ template <int V, bool FULL>
 __global__ __launch_bounds__(256) void pair_final2_kernel(PairArgs a0, PairArgs a1, Geom g) {
     constexpr int K = pair_kv<V>();
     __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
-    const PairArgs &a = __builtin_amdgcn_workgroup_id_z() != 0 ? a1 : a0;
+    const PairArgs a = __builtin_amdgcn_workgroup_id_z() != 0 ? a1 : a0;
     pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>()>(
         a, g, bid_x(), wave_id(), lds.s, &lds);
 }
@@ -252,8 +252,8 @@ __global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, P
     constexpr int PFH = V >= 4 ? 16 : 32;
 #endif
     const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
-    const PairArgs &h1 = vb ? h1b : h1a;
-    const PairArgs &h2 = vb ? h2b : h2a;
+    const PairArgs h1 = vb ? h1b : h1a;
+    const PairArgs h2 = vb ? h2b : h2a;
     pair_fwd_body<0, V, FULL, PFH>(h1, g, bid_x());
     __threadfence();  // this wave's checkpoint stores, before it reads them back
     pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, bid_x(), nullptr, nullptr);
