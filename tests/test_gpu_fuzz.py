@@ -50,14 +50,19 @@ def test_random_frame(c, split, monkeypatch):
 
 
 @pytest.mark.parametrize("c", CASES, ids=[f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_V{c['views']}" for c in CASES])
-@pytest.mark.parametrize("fwd", ["1", "0"], ids=["fwdbands", "bwdbands"])
+@pytest.mark.parametrize("fwd", ["1", "0", "mixed"], ids=["fwdbands", "bwdbands", "mixed"])
 def test_random_frame_banded(c, fwd, monkeypatch):
     """16-row bands (the schedule of volumes above the Infinity Cache): the
     forward phase (vfwd, L5, L6) band by band top down, both views' H pairs
     in one launch, then the backward phase (stage B's diagonal pair, L8 and
     the final pass) band by band bottom up, chain and filter states carried
-    across band edges; SGM_FWD_BANDS=0 keeps the forward phase whole."""
+    across band edges; SGM_FWD_BANDS=0 keeps the forward phase whole, and
+    "mixed" runs 16-row forward bands with 32-row backward bands."""
     monkeypatch.setenv("SGM_BAND_ROWS", "16")
+    if fwd == "mixed":  # forward and backward bands of different sizes
+        monkeypatch.setenv("SGM_BAND_ROWS", "32")
+        monkeypatch.setenv("SGM_FWD_BAND_ROWS", "16")
+        fwd = "1"
     monkeypatch.setenv("SGM_FWD_BANDS", fwd)
     _check(c)
 
