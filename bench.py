@@ -35,6 +35,10 @@ METRIC = "Mpixel-disparities/s, 8-path SGM @ KITTI 1242×375 D=128; 1→8 GPU sc
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 
 CONFIGS = {
+    # BASELINE.json configs[0] ("config 1"): the reference's CPU-runnable case;
+    # here both the GPU path and the CPU baseline run it
+    "k64": dict(h=375, w=1242, D=64, views=2,
+                workload="config1: KITTI 1242x375 D=64, both views + LR check (V=2), 1 pair per GPU"),
     "k128": dict(h=375, w=1242, D=128, views=1,
                  workload="config2: KITTI 1242x375 D=128, census 9x7 + Hamming cost + 8-path "
                           "SGM + WTA/uniqueness/sub-pixel, left view (V=1), 1 pair per GPU"),
@@ -84,6 +88,33 @@ def bytes_per_elem(name: str, D: int) -> float:
     if name.startswith("sweep_"):
         return {"init": 8.0, "acc": 12.0, "final": 12.0, "store": 8.0}[name.rsplit("_", 1)[1]]
     return 0.0
+
+
+# Of those bytes, the reads of the final cost volume C (4 B per element per
+# path direction that walks it).  At K128/K64 C (238.5 / 119 MB) stays in the
+# 256 MB Infinity Cache through the aggregation (DESIGN.md "Infinity Cache"),
+# so algorithmic bytes minus these are the bytes the kernel moves to/from HBM.
+def c_read_bytes_per_elem(name: str) -> float:
+    table = {"stage_a": 12.0, "stage_b": 8.0, "pair_bwd_L4_final": 4.0, "sweep_L8_acc": 4.0,
+             "stage_a_hp": 16.0, "stage_b_d2": 4.0, "stage_a_d": 8.0, "stage_a_h": 8.0,
+             "pair_fwd_L1": 4.0, "pair_fwd_L3": 4.0, "pair_fwd_L6": 4.0,
+             "pair_bwd_L2_init2": 4.0, "pair_bwd_L7_acc": 4.0}
+    if name in table:
+        return table[name]
+    return 4.0 if name.startswith("sweep_") else 0.0
+
+
+def source_sha() -> str:
+    """sha256 (first 16 hex digits) over the library's sources: ties a PMC
+    traffic record (profiles/pmc_traffic.json) to the code it was taken on."""
+    import hashlib
+    csrc = os.path.join(ROOT, "stereo_matching_amd", "csrc")
+    hsh = hashlib.sha256()
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")) or f == "Makefile":
+            with open(os.path.join(csrc, f), "rb") as fh:
+                hsh.update(f.encode() + b"\0" + fh.read())
+    return hsh.hexdigest()[:16]
 
 
 BYTES_PER_PIXEL = {"census": 9, "lr": 12,
@@ -160,7 +191,10 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # under torch.distributed.run (the driver's launch line for N > 1, and the
+    # GPU test of that line at N = 1) the process group comes up on RCCL
+    distributed = world > 1 or "LOCAL_WORLD_SIZE" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
     if args.view_split and (world % 2 or views != 2):
         raise SystemExit("--view-split needs an even number of ranks and a two-view config")
@@ -176,7 +210,7 @@ def main():
     # N > 1: each step's map goes to rank 0 by a gather that overlaps the next
     # step's kernels (double-buffered maps, stereo_matching_amd.distributed)
     pipe = None
-    if world > 1 and not args.view_split:
+    if distributed and not args.view_split:
         from stereo_matching_amd.distributed import PipelinedGather
         pipe = PipelinedGather((h, w), torch.float32, dev, depth=2)
 
@@ -210,7 +244,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     def timed_steps(k):
-        if world > 1:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -219,12 +253,12 @@ def main():
         if pipe:
             pipe.drain()  # every gather of the timed steps is inside the timed region
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if distributed:
             dist.barrier()
         return time.perf_counter() - t0
 
     elapsed = timed_steps(args.steps)
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -239,7 +273,7 @@ def main():
     kernels = {}
     if not args.no_profile_pass:
         sgm.set_profiling(True)
-        timed_steps(args.steps)
+        prof_elapsed = timed_steps(args.steps)
         prof = sgm.get_profile()
         sgm.set_profiling(False)
         for name, (n, total_ms, elems) in prof.items():
@@ -258,10 +292,38 @@ def main():
                         traffic = json.load(fh).get(args.config, {}).get(dom)
                 except (OSError, ValueError):
                     traffic = None
+            tag = pmc_tag = None
+            src = source_sha()
+            if traffic is not None:
+                with open(pmc) as fh:
+                    pmc_tag = json.load(fh).get("_tags", {}).get(args.config)
+                tag = pmc_tag.get("tag") if isinstance(pmc_tag, dict) else pmc_tag
+            # streams only: without the reads of C, which the Infinity Cache
+            # serves when the volume fits it (K64/K128); above it they are HBM
+            # reads too and frac is already the HBM figure
+            fits = h * w * D * 4 <= (256 << 20)
+            cbytes = c_read_bytes_per_elem(dom) * kd["algo_bytes"] / max(bytes_per_elem(dom, D), 1e-9) \
+                if fits and bytes_per_elem(dom, D) else 0.0
+            streams = (kd["algo_bytes"] - cbytes) / (kd["avg_us"] * 1e-6) / 1e9
+            kernel_sum_ms = sum(v["share_per_step_ms"] for v in kernels.values())
             roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "algo_bytes_per_launch": kd["algo_bytes"], "avg_launch_us": kd["avg_us"]}
+                        "traffic_tag": tag,
+                        "traffic_src_sha": pmc_tag.get("src_sha") if isinstance(pmc_tag, dict) else None,
+                        "src_sha": src,
+                        "traffic_matches_source": bool(isinstance(pmc_tag, dict)
+                                                       and pmc_tag.get("src_sha") == src),
+                        "algo_bytes_per_launch": kd["algo_bytes"], "avg_launch_us": kd["avg_us"],
+                        # HBM-only view: C reads served by the Infinity Cache left out
+                        "c_cache_resident": fits,
+                        "achieved_hbm_only": round(streams, 1),
+                        "frac_hbm_only": round(streams / HBM_PEAK_GBS, 4),
+                        # per-kernel times come from a second, event-bracketed pass;
+                        # flag when its kernel sum exceeds the timed step
+                        "kernel_sum_ms_per_step": round(kernel_sum_ms, 4),
+                        "profile_pass_ms_per_step": round(prof_elapsed / args.steps * 1e3, 4),
+                        "kernel_sum_exceeds_timed_step": kernel_sum_ms > ms_per_step}
             # the 8-path aggregation kernels (everything after the cost volume
             # except vfwd, which is mostly the vertical cost filter)
             agg = [k for k in kernels if k.startswith(("sweep_", "pair_", "stage_"))]
@@ -298,10 +360,17 @@ def main():
                    "scope": "sgm_process: H2D images, pipeline, D2H disparity, synchronous"}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    cpu_note = None
+    if world > 1:
+        cpu_note = ("measured on rank 0 at N=1 only (bench contract); the N=1 line of the same "
+                    "config carries it")
+    elif rank == 0 and not args.no_cpu_baseline:
         import oracle
         oracle.build()
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        # every host thread this process may use: OMP_NUM_THREADS when the
+        # environment sets it (the GPU pool sets it to the box's CPU share),
+        # else all host CPUs
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
         oracle.set_threads(threads)
         # bounded sample (~0.6 G pixel-disparity units per frame): a band of the
         # frame's top rows at full width when the frame is larger than that
@@ -313,7 +382,7 @@ def main():
             t0 = time.perf_counter()
             ml = oracle.sky_detect(ls) if full else None
             mr = oracle.sky_detect(rs) if full else None
-            ref = oracle.process(ls, rs, D, views=views, sky_l=ml, sky_r=mr)
+            ref = oracle.process(ls, rs, D, views=views, sky_l=ml, sky_r=mr, schedule="refplace")
             if full:
                 oracle.lk_refine(ls, rs, ref["final"], D)
             ts.append(time.perf_counter() - t0)
@@ -321,11 +390,19 @@ def main():
         what = "full frames" if sh == h else f"bands of the top {sh} rows (full width)"
         stages = ("sky detector + SGM + LR + post_filter + LKRefine" if full else
                   "SGM" + (" + LR + post_filter" if views == 2 else ""))
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            affinity = None
         cpu = {"value": round(views * sh * w * D / tmed / 1e6, 2), "unit": "Mpixel-disparities/s",
-               "cores": oracle.max_threads(), "kind": "port", "cpu_model": cpu_model(),
+               "cores": oracle.max_threads(), "kind": "port", "placement": "reference",
+               "omp_max_threads": oracle.max_threads(), "host_cpus": os.cpu_count(),
+               "affinity_cpus": affinity, "cpu_model": cpu_model(),
                "sample": f"{len(ts)} {what} of the same workload ({w}x{h} D={D}, V={views}; "
-                         f"{stages}) through oracle/sgm_oracle.c (C restatement, OpenMP "
-                         f"placement of the reference), median {tmed:.3f} s per sample"}
+                         f"{stages}) through orc_process_refplace (oracle/sgm_oracle.c): the "
+                         f"reference's loop nests and OpenMP placement -- parallel only at its "
+                         f"`omp parallel for` sites, both cost filters and the aggregation + WTA "
+                         f"sequential, 10 volumes -- median {tmed:.3f} s per sample"}
 
     if rank == 0:
         rec = {
@@ -346,13 +423,16 @@ def main():
                                        f"RCCL point-to-point; maps stay on the even ranks)"
                                        if args.view_split else
                                        f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0 "
-                                       f"overlapped with the next step")},
+                                       f"overlapped with the next step" if distributed else
+                                       "1 pair on 1 GPU (single process: no process group, no "
+                                       "gather)")},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+            **({"cpu_baseline_note": cpu_note} if cpu_note else {}),
             "host_io": host_io,
         }
         print(json.dumps(rec))
     sgm.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

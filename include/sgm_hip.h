@@ -171,11 +171,6 @@ int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_ri
 int sgm_lr_check_device(sgm_handle *h, const float *d_fl, int fl_pitch, const float *d_fr,
                         int fr_pitch, float *d_out, int out_pitch, void *stream);
 
-/* post_filter() (Solver.cpp:600-649) on a host rows x cols f32 map, in place:
- * 5x5 median fill + speckle removal, single-thread semantics, on the host CPU
- * (kept for callers without a handle; the GPU entry points below replace it). */
-int sgm_post_filter_host(float *disp, int rows, int cols, int max_disp, int scale);
-
 /* post_filter() (Solver.cpp:600-649: median fill :604-630, speckle_filter_new
  * :514-566) on the GPU, bit-exact against its single-thread semantics, in
  * place on a DEVICE map of the handle's working size (rows x cols f32, row

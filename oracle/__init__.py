@@ -61,6 +61,9 @@ def lib():
         L.orc_bm_process.restype = I
         L.orc_process.argtypes = [P, P, P, P, I, I, I, I, I, I, F, F, I, I, ctypes.POINTER(_Result)]
         L.orc_process.restype = I
+        for fn in (L.orc_process_lean, L.orc_process_refplace):
+            fn.argtypes = L.orc_process.argtypes
+            fn.restype = I
         L.orc_max_threads.restype = I
         L.orc_set_threads.argtypes = [I]
         _lib = L
@@ -198,9 +201,17 @@ def bm_process(left, right, D, scale=1, sky=None, uniq=0.7, blur=True):
     return disp
 
 
+_SCHEDULES = {"parity": "orc_process", "lean": "orc_process_lean",
+              "refplace": "orc_process_refplace"}
+
+
 def process(left, right, D, scale=1, sky_l=None, sky_r=None, P1=10, P2=100,
-            uniq=0.7, lr_dis=1.0, blur=True, views=2):
-    """Whole SGM::process (src/SGM.cpp:32-826).  Returns a dict of HW arrays."""
+            uniq=0.7, lr_dis=1.0, blur=True, views=2, schedule="parity", final=True):
+    """Whole SGM::process (src/SGM.cpp:32-826).  Returns a dict of HW arrays.
+
+    schedule: "parity" (10 volumes), "lean" (3 volumes, for 4K256) or
+    "refplace" (the reference's OpenMP placement, the timed CPU baseline);
+    all three give identical bits.  final=False skips post_filter."""
     left = _c(left, np.uint8)
     right = _c(right, np.uint8)
     h, w = left.shape
@@ -210,10 +221,12 @@ def process(left, right, D, scale=1, sky_l=None, sky_r=None, P1=10, P2=100,
     out = {"disp": np.empty((H, W), np.int32), "sub": np.empty((H, W), np.float32)}
     if views >= 2:
         out.update(disp_beta=np.empty((H, W), np.int32), sub_beta=np.empty((H, W), np.float32),
-                   lr=np.empty((H, W), np.float32), final=np.empty((H, W), np.float32))
+                   lr=np.empty((H, W), np.float32))
+        if final:
+            out["final"] = np.empty((H, W), np.float32)
     r = _Result(_p(out["disp"]), _p(out.get("disp_beta")), _p(out["sub"]),
                 _p(out.get("sub_beta")), _p(out.get("lr")), _p(out.get("final")))
-    rc = lib().orc_process(_p(left), _p(right), _p(sky_l), _p(sky_r), h, w, scale, D, P1, P2,
+    rc = getattr(lib(), _SCHEDULES[schedule])(_p(left), _p(right), _p(sky_l), _p(sky_r), h, w, scale, D, P1, P2,
                            uniq, lr_dis, int(bool(blur)), views, ctypes.byref(r))
     if rc != 0:
         raise ValueError("orc_process rejected its arguments")

@@ -9,9 +9,17 @@
  * (needs OpenCV + ROS headers, inc/global.h:11-20) and ships no golden
  * vectors; see sgm_oracle.h and DESIGN.md section "Oracle".
  *
- * OpenMP placement mirrors the reference so the timed
- * baseline has the reference's parallel structure; every parallel loop writes
- * disjoint outputs, so results do not depend on the thread count.
+ * Three schedules of the same arithmetic, bit-identical outputs:
+ *  - orc_process: per-stage functions with 10 volumes (cost, S, L1..L8), the
+ *    parity checker at sizes up to HD256.  It parallelises loops the
+ *    reference runs sequentially (both cost filters, the aggregation), since
+ *    their rows/columns are independent; it is NOT the reference's placement.
+ *  - orc_process_lean: 3 volumes, streamed path states (4K256 parity).
+ *  - orc_process_refplace: the reference's OpenMP placement (parallel only at
+ *    its `omp parallel for` sites; filters and aggregation + WTA sequential),
+ *    the timed CPU baseline of bench.py.
+ * Every parallel loop writes disjoint outputs, so results do not depend on
+ * the thread count.
  */
 #include "sgm_oracle.h"
 
@@ -156,10 +164,10 @@ void orc_dsi(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
 
 /* cost_horizontal_filter, src/Solver.cpp:296-330, literally (sequential in
  * the reference; rows are independent so the restatement may parallelise). */
-void orc_hfilter(float *cost, int H, int W, int D, int win)
+static void hfilter_impl(float *cost, int H, int W, int D, int win, int par)
 {
     const i64 index_step = (i64)(win / 2 + 1) * D;
-#pragma omp parallel for
+#pragma omp parallel for if (par)
     for (int i = 0; i < H; ++i) {
         for (int d = 0; d < D; ++d) {
             float sum = 0;
@@ -180,11 +188,11 @@ void orc_hfilter(float *cost, int H, int W, int D, int win)
 }
 
 /* cost_vertical_filter, src/Solver.cpp:333-368, literally. */
-void orc_vfilter(float *cost, int H, int W, int D, int win)
+static void vfilter_impl(float *cost, int H, int W, int D, int win, int par)
 {
     const i64 step = (i64)W * D;
     const i64 index_step = (i64)(win / 2 + 1) * step;
-#pragma omp parallel for
+#pragma omp parallel for if (par)
     for (int j = 0; j < W; ++j) {
         for (int d = 0; d < D; ++d) {
             float sum = 0;
@@ -204,29 +212,53 @@ void orc_vfilter(float *cost, int H, int W, int D, int win)
     }
 }
 
+void orc_hfilter(float *cost, int H, int W, int D, int win) { hfilter_impl(cost, H, W, D, win, 1); }
+void orc_vfilter(float *cost, int H, int W, int D, int win) { vfilter_impl(cost, H, W, D, win, 1); }
+
 /* ---------------------------------------------------------- path DPs */
 
 /* One pixel of one path, src/SGM.cpp:93-117 (identical body in all eight
- * directions): prev == NULL means the path starts here. */
+ * directions): prev == NULL means the path starts here.  The d loop is split
+ * into its two clamped ends and a clamp-free interior, and the minimum is
+ * taken over 8 interleaved partial minima, so that the compiler vectorises
+ * both; the values are unchanged (every L is >= 0 and finite, and a minimum
+ * of such values does not depend on the order it is taken in). */
+static inline float dp_one(const float *prev, int d, int dm, int dp, float P1, float base,
+                           float cd, float min_prev)
+{
+    float v = ORC_MIN(prev[d], prev[dm] + P1);
+    v = ORC_MIN(v, prev[dp] + P1);
+    v = ORC_MIN(v, base);
+    return v + (cd - min_prev);
+}
+
 static inline void dp_pixel(const float *c, float *l, const float *prev, float min_prev,
                             int D, float P1, float P2, float *min_out)
 {
-    float m = FLT_MAX;
-    for (int d = 0; d < D; ++d) {
-        int d_sub_1 = ORC_MAX(d - 1, 0);
-        int d_plus_1 = ORC_MIN(d + 1, D - 1);
-        float v;
-        if (!prev) {
-            v = c[d];
-        } else {
-            v = ORC_MIN(prev[d], prev[d_sub_1] + P1);
-            v = ORC_MIN(v, prev[d_plus_1] + P1);
-            v = ORC_MIN(v, min_prev + P2);
-            v += (c[d] - min_prev);
+    if (!prev) {
+        for (int d = 0; d < D; ++d) l[d] = c[d];
+    } else if (D < 3) {
+        for (int d = 0; d < D; ++d)
+            l[d] = dp_one(prev, d, ORC_MAX(d - 1, 0), ORC_MIN(d + 1, D - 1), P1, min_prev + P2,
+                          c[d], min_prev);
+    } else {
+        const float base = min_prev + P2;
+        l[0] = dp_one(prev, 0, 0, 1, P1, base, c[0], min_prev);
+        for (int d = 1; d < D - 1; ++d) {
+            float v = ORC_MIN(prev[d], prev[d - 1] + P1);
+            v = ORC_MIN(v, prev[d + 1] + P1);
+            v = ORC_MIN(v, base);
+            l[d] = v + (c[d] - min_prev);
         }
-        l[d] = v;
-        if (v < m) m = v;
+        l[D - 1] = dp_one(prev, D - 1, D - 2, D - 1, P1, base, c[D - 1], min_prev);
     }
+    float m8[8] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+    int d = 0;
+    for (; d + 8 <= D; d += 8)
+        for (int k = 0; k < 8; ++k) m8[k] = l[d + k] < m8[k] ? l[d + k] : m8[k];
+    float m = FLT_MAX;
+    for (; d < D; ++d) m = l[d] < m ? l[d] : m;
+    for (int k = 0; k < 8; ++k) m = m8[k] < m ? m8[k] : m;
     *min_out = m;
 }
 
@@ -369,7 +401,14 @@ void orc_subpixel(const int32_t *disp, const float *S, float *out, int H, int W,
     }
 }
 
-/* src/SGM.cpp:803-818. */
+/* src/SGM.cpp:803-818.
+ * The column read FR(i, (int)(j - dl/s)) is clamped to [0, W-1], as the GPU's
+ * lr_kernel does.  For every map compute_subpixel can produce the clamp never
+ * acts: dl is NaN (j >= NaN is false), D+1, an integer d, min(+inf, D-1) or a
+ * parabola vertex in [d-1/2, d+1/2] (DESIGN.md "LR check domain"), so
+ * 0 <= (int)(j - dl/s) <= j.  It only matters for arbitrary maps handed to the
+ * stage entry points, where the reference's cv::Mat::at reads a neighbouring
+ * row (or outside the buffer, undefined); the clamp is this build's choice. */
 void orc_lr_check(float *FL, const float *FR, int H, int W, int D, int scale, float lr_dis)
 {
     const float invalid = (float)(D + 1);
@@ -378,7 +417,9 @@ void orc_lr_check(float *FL, const float *FR, int H, int W, int D, int scale, fl
         for (int j = 0; j < W; ++j) {
             float *dl = FL + (i64)i * W + j;
             if (j >= *dl) {
-                int jr = (int)(j - *dl / scale);
+                const float x = j - *dl / scale;   /* clamped before the int
+                                                      conversion: defined for any dl */
+                const int jr = x < 0 ? 0 : (x > (float)(W - 1) ? W - 1 : (int)x);
                 float dr = FR[(i64)i * W + jr];
                 if (fabsf(*dl - dr) > lr_dis) *dl = invalid;
             }
@@ -489,7 +530,9 @@ void orc_lk_refine(const uint8_t *L, const uint8_t *R, float *disp, int H, int W
             nd[k] = (float)(int)disp[k];
             dt[k] = (float)(int)disp[k];
         }
-    /* per-pixel Gauss-Newton on the disparity offset (:86-233) */
+    /* per-pixel Gauss-Newton on the disparity offset (:86-233); pixels are
+     * independent (each reads dt/Ix/L/R, writes only its own nd) */
+#pragma omp parallel for schedule(dynamic, 4)
     for (int i = hw; i < H - hw; ++i) {
         for (int j = hw; j < W - hw; ++j) {
             const i64 c = (i64)i * W + j;
@@ -744,17 +787,215 @@ int orc_bm_process(const uint8_t *left, const uint8_t *right, const uint8_t *sky
     return 0;
 }
 
+/* ------------------------------------------------------ lean schedule */
+
+/* The same per-view result as orc_path x 8 + orc_aggregate + orc_wta +
+ * orc_subpixel, holding 3 volumes (C, S, T) instead of 10: every path
+ * streams its chain state (one D-vector per chain; the diagonal passes keep
+ * the previous row's W states) and adds into an accumulator in the
+ * reference's association order (src/SGM.cpp:386-390):
+ *     S = L1; S += L2; S += L3; S += L4          -> ((L1+L2)+L3)+L4
+ *     T = L5 + L6 (one top-down pass, as SGM.cpp:247-305 computes L5, L6)
+ *     S += (T + L7) + L8 (one bottom-up pass, as SGM.cpp:311-369)
+ * IEEE addition is commutative, so S + L2 == L1 + L2 bit for bit.  At 4K256
+ * that is 3 x 8.5 GB instead of 10 x 8.5 GB (tests/test_oracle.py proves it
+ * identical to orc_process on the golden and fuzz shapes). */
+static void lean_rows(const float *C, float *S, int H, int W, int D, float P1, float P2)
+{
+#pragma omp parallel
+    {
+        float *a = (float *)malloc(sizeof(float) * (size_t)D);
+        float *b = (float *)malloc(sizeof(float) * (size_t)D);
+#pragma omp for schedule(dynamic, 1)
+        for (int i = 0; i < H; ++i) {
+            float *prev = a, *cur = b, mp = 0.f, m;
+            for (int j = 0; j < W; ++j) {                    /* L1, SGM.cpp:82-119 */
+                const i64 q = ((i64)i * W + j) * D;
+                dp_pixel(C + q, cur, j == 0 ? NULL : prev, mp, D, P1, P2, &m);
+                memcpy(S + q, cur, sizeof(float) * (size_t)D);
+                float *t = prev; prev = cur; cur = t; mp = m;
+            }
+            for (int j = W - 1; j >= 0; --j) {               /* L2, SGM.cpp:122-159 */
+                const i64 q = ((i64)i * W + j) * D;
+                dp_pixel(C + q, cur, j == W - 1 ? NULL : prev, mp, D, P1, P2, &m);
+                for (int d = 0; d < D; ++d) S[q + d] = S[q + d] + cur[d];
+                float *t = prev; prev = cur; cur = t; mp = m;
+            }
+        }
+        free(a);
+        free(b);
+    }
+}
+
+static void lean_cols(const float *C, float *S, int H, int W, int D, float P1, float P2)
+{
+#pragma omp parallel
+    {
+        float *a = (float *)malloc(sizeof(float) * (size_t)D);
+        float *b = (float *)malloc(sizeof(float) * (size_t)D);
+#pragma omp for schedule(dynamic, 4)
+        for (int j = 0; j < W; ++j) {
+            float *prev = a, *cur = b, mp = 0.f, m;
+            for (int i = 0; i < H; ++i) {                    /* L3, SGM.cpp:162-199 */
+                const i64 q = ((i64)i * W + j) * D;
+                dp_pixel(C + q, cur, i == 0 ? NULL : prev, mp, D, P1, P2, &m);
+                for (int d = 0; d < D; ++d) S[q + d] = S[q + d] + cur[d];
+                float *t = prev; prev = cur; cur = t; mp = m;
+            }
+            for (int i = H - 1; i >= 0; --i) {               /* L4, SGM.cpp:202-239 */
+                const i64 q = ((i64)i * W + j) * D;
+                dp_pixel(C + q, cur, i == H - 1 ? NULL : prev, mp, D, P1, P2, &m);
+                for (int d = 0; d < D; ++d) S[q + d] = S[q + d] + cur[d];
+                float *t = prev; prev = cur; cur = t; mp = m;
+            }
+        }
+        free(a);
+        free(b);
+    }
+}
+
+/* Both diagonal pairs.  down = 1: L5 (i-1, j-1) and L6 (i-1, j+1), T = L5+L6.
+ * down = 0: L7 (i+1, j-1) and L8 (i+1, j+1), S += (T + L7) + L8. */
+static void lean_diag(const float *C, float *S, float *T, int H, int W, int D, float P1,
+                      float P2, int down)
+{
+    const i64 row = (i64)W * D;
+    float *pa = (float *)malloc(sizeof(float) * (size_t)row), *ca = (float *)malloc(sizeof(float) * (size_t)row);
+    float *pb = (float *)malloc(sizeof(float) * (size_t)row), *cb = (float *)malloc(sizeof(float) * (size_t)row);
+    float *ma = (float *)malloc(sizeof(float) * (size_t)W), *na = (float *)malloc(sizeof(float) * (size_t)W);
+    float *mb = (float *)malloc(sizeof(float) * (size_t)W), *nb = (float *)malloc(sizeof(float) * (size_t)W);
+    for (int k = 0; k < H; ++k) {
+        const int i = down ? k : H - 1 - k;
+        const int first = k == 0;
+#pragma omp parallel for schedule(static)
+        for (int j = 0; j < W; ++j) {
+            const i64 q = ((i64)i * W + j) * D;
+            float *la = ca + (i64)j * D, *lb = cb + (i64)j * D;
+            /* path a comes from column j-1 (L5 / L7), path b from j+1 (L6 / L8) */
+            if (first || j == 0) dp_pixel(C + q, la, NULL, 0.f, D, P1, P2, na + j);
+            else dp_pixel(C + q, la, pa + (i64)(j - 1) * D, ma[j - 1], D, P1, P2, na + j);
+            if (first || j == W - 1) dp_pixel(C + q, lb, NULL, 0.f, D, P1, P2, nb + j);
+            else dp_pixel(C + q, lb, pb + (i64)(j + 1) * D, mb[j + 1], D, P1, P2, nb + j);
+            if (down) {
+                for (int d = 0; d < D; ++d) T[q + d] = la[d] + lb[d];
+            } else {
+                for (int d = 0; d < D; ++d) S[q + d] = S[q + d] + ((T[q + d] + la[d]) + lb[d]);
+            }
+        }
+        float *t;
+        t = pa; pa = ca; ca = t;
+        t = pb; pb = cb; cb = t;
+        t = ma; ma = na; na = t;
+        t = mb; mb = nb; nb = t;
+    }
+    free(pa); free(ca); free(pb); free(cb); free(ma); free(na); free(mb); free(nb);
+}
+
+/* orc_wta's result computed per pixel in parallel: the reference's sec_min_d
+ * persists from the previous pixel in raster order when every cost equals the
+ * minimum (SGM.cpp:374-375, 398-407), so pixels without a second minimum take
+ * it from the last earlier pixel that had one, in a sequential pass. */
+static void wta_par(const float *S, int32_t *disp, int H, int W, int D, float uniq)
+{
+    const int invalid = D + 1;
+    const i64 n = (i64)H * W;
+    int32_t *mind = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    int32_t *secd = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    float *ratio = (float *)malloc(sizeof(float) * (size_t)n);
+#pragma omp parallel for schedule(static)
+    for (i64 p = 0; p < n; ++p) {
+        const float *s = S + p * D;
+        float mc = FLT_MAX, sc = FLT_MAX;
+        int md = invalid, sd = -1;
+        for (int d = 0; d < D; ++d)
+            if (s[d] < mc) { mc = s[d]; md = d; }
+        for (int d = 0; d < D; ++d)
+            if (s[d] < sc && s[d] != mc) { sc = s[d]; sd = d; }
+        mind[p] = md;
+        secd[p] = sd;
+        ratio[p] = mc / sc;
+    }
+    int last = invalid;
+    for (i64 p = 0; p < n; ++p) {
+        if (secd[p] >= 0) last = secd[p];
+        disp[p] = (ratio[p] > uniq && abs(mind[p] - last) > 1) ? invalid : mind[p];
+    }
+    free(mind);
+    free(secd);
+    free(ratio);
+}
+
+/* ------------------------------------- the reference's OpenMP placement */
+
+/* L5/L6 and L7/L8 as the reference computes them: one row loop per pair,
+ * rows in order, omp over the columns of a row (SGM.cpp:247-305, 311-369). */
+static void refplace_diag_pair(const float *C, float *La, float *Lb, float *ma, float *mb,
+                               int H, int W, int D, float P1, float P2, int down)
+{
+    for (int k = 0; k < H; ++k) {
+        const int i = down ? k : H - 1 - k;
+        const int pi = down ? i - 1 : i + 1;
+        const int edge = k == 0;
+#pragma omp parallel for
+        for (int j = 0; j < W; ++j) {
+            const i64 q = (i64)i * W + j;
+            if (edge || j == 0) dp_pixel(C + q * D, La + q * D, NULL, 0.f, D, P1, P2, ma + q);
+            else {
+                const i64 p = (i64)pi * W + j - 1;
+                dp_pixel(C + q * D, La + q * D, La + p * D, ma[p], D, P1, P2, ma + q);
+            }
+            if (edge || j == W - 1) dp_pixel(C + q * D, Lb + q * D, NULL, 0.f, D, P1, P2, mb + q);
+            else {
+                const i64 p = (i64)pi * W + j + 1;
+                dp_pixel(C + q * D, Lb + q * D, Lb + p * D, mb[p], D, P1, P2, mb + q);
+            }
+        }
+    }
+}
+
+/* Aggregation + WTA + uniqueness fused and sequential, as SGM.cpp:372-418
+ * (the sum is written over cost there; here into S). */
+static void refplace_agg_wta(float *const *L, float *S, int32_t *disp, int H, int W, int D,
+                             float uniq)
+{
+    const int invalid = D + 1;
+    float min_cost = FLT_MAX, sec_min_cost = FLT_MAX;
+    int min_d = invalid, sec_min_d = invalid;
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            min_cost = FLT_MAX;
+            const i64 b = ((i64)i * W + j) * D;
+            for (int d = 0; d < D; ++d) {
+                const i64 k = b + d;
+                S[k] = L[0][k] + L[1][k] + L[2][k] + L[3][k];
+                S[k] += (L[4][k] + L[5][k] + L[6][k] + L[7][k]);
+                if (S[k] < min_cost) { min_cost = S[k]; min_d = d; }
+            }
+            sec_min_cost = FLT_MAX;
+            for (int d = 0; d < D; ++d)
+                if (S[b + d] < sec_min_cost && S[b + d] != min_cost) {
+                    sec_min_cost = S[b + d];
+                    sec_min_d = d;
+                }
+            disp[(i64)i * W + j] =
+                (min_cost / sec_min_cost > uniq && abs(min_d - sec_min_d) > 1) ? invalid : min_d;
+        }
+}
+
 /* --------------------------------------------------------- whole process */
 
-int orc_process(const uint8_t *left, const uint8_t *right,
-                const uint8_t *sky_l, const uint8_t *sky_r,
-                int h, int w, int scale, int D, int P1, int P2,
-                float uniq, float lr_dis, int blur, int views, orc_result *res)
+enum { MODE_PARITY = 0, MODE_LEAN = 1, MODE_REFPLACE = 2 };
+
+static int process_mode(const uint8_t *left, const uint8_t *right,
+                        const uint8_t *sky_l, const uint8_t *sky_r,
+                        int h, int w, int scale, int D, int P1i, int P2i,
+                        float uniq, float lr_dis, int blur, int views, orc_result *res, int mode)
 {
     if (h <= 0 || w <= 0 || (scale != 1 && scale != 2) || D <= 0) return -1;
     const int H = h / scale, W = w / scale;
     const i64 npx = (i64)H * W, nvol = npx * D;
     if (W < 5 || H < 3) return -1;
+    const float P1 = (float)P1i, P2 = (float)P2i;
 
     uint8_t *l = (uint8_t *)malloc((size_t)npx), *r = (uint8_t *)malloc((size_t)npx);
     /* decimation, src/SGM.cpp:40-61 */
@@ -778,10 +1019,15 @@ int orc_process(const uint8_t *left, const uint8_t *right,
 
     float *cost = (float *)malloc(sizeof(float) * (size_t)nvol);
     float *S = (float *)malloc(sizeof(float) * (size_t)nvol);
-    float *Ls[8], *mins[8];
-    for (int k = 0; k < 8; ++k) {
-        Ls[k] = (float *)malloc(sizeof(float) * (size_t)nvol);
-        mins[k] = (float *)malloc(sizeof(float) * (size_t)npx);
+    float *T = NULL;
+    float *Ls[8] = {0}, *mins[8] = {0};
+    if (mode == MODE_LEAN) {
+        T = (float *)malloc(sizeof(float) * (size_t)nvol);
+    } else {
+        for (int k = 0; k < 8; ++k) {
+            Ls[k] = (float *)malloc(sizeof(float) * (size_t)nvol);
+            mins[k] = (float *)malloc(sizeof(float) * (size_t)npx);
+        }
     }
     int32_t *disp = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx);
     int32_t *disp_b = (int32_t *)malloc(sizeof(int32_t) * (size_t)npx);
@@ -789,13 +1035,28 @@ int orc_process(const uint8_t *left, const uint8_t *right,
     float *sub_b = (float *)malloc(sizeof(float) * (size_t)npx);
 
     for (int view = 0; view < (views >= 2 ? 2 : 1); ++view) {
+        int32_t *dv = view == 0 ? disp : disp_b;
         orc_dsi(ctl, ctr, view == 0 ? sky_l : sky_r, cost, H, W, D, scale, view);
-        orc_hfilter(cost, H, W, D, 5 / scale);
-        orc_vfilter(cost, H, W, D, 3 / scale);
-        for (int k = 0; k < 8; ++k) orc_path(cost, Ls[k], mins[k], H, W, D, k, P1, P2);
-        orc_aggregate((const float *const *)Ls, S, H, W, D);
-        orc_wta(S, view == 0 ? disp : disp_b, H, W, D, uniq);
-        orc_subpixel(view == 0 ? disp : disp_b, S, view == 0 ? sub : sub_b, H, W, D);
+        /* the reference runs both filters sequentially (Solver.cpp:296-368) */
+        hfilter_impl(cost, H, W, D, 5 / scale, mode != MODE_REFPLACE);
+        vfilter_impl(cost, H, W, D, 3 / scale, mode != MODE_REFPLACE);
+        if (mode == MODE_LEAN) {
+            lean_rows(cost, S, H, W, D, P1, P2);
+            lean_cols(cost, S, H, W, D, P1, P2);
+            lean_diag(cost, S, T, H, W, D, P1, P2, 1);
+            lean_diag(cost, S, T, H, W, D, P1, P2, 0);
+            wta_par(S, dv, H, W, D, uniq);
+        } else if (mode == MODE_REFPLACE) {
+            for (int k = 0; k < 4; ++k) orc_path(cost, Ls[k], mins[k], H, W, D, k, P1i, P2i);
+            refplace_diag_pair(cost, Ls[4], Ls[5], mins[4], mins[5], H, W, D, P1, P2, 1);
+            refplace_diag_pair(cost, Ls[6], Ls[7], mins[6], mins[7], H, W, D, P1, P2, 0);
+            refplace_agg_wta(Ls, S, dv, H, W, D, uniq);
+        } else {
+            for (int k = 0; k < 8; ++k) orc_path(cost, Ls[k], mins[k], H, W, D, k, P1i, P2i);
+            orc_aggregate((const float *const *)Ls, S, H, W, D);
+            orc_wta(S, dv, H, W, D, uniq);
+        }
+        orc_subpixel(dv, S, view == 0 ? sub : sub_b, H, W, D);
     }
 
     if (res) {
@@ -820,9 +1081,37 @@ int orc_process(const uint8_t *left, const uint8_t *right,
         free(Ls[k]);
         free(mins[k]);
     }
+    free(T);
     free(cost); free(S); free(disp); free(disp_b); free(sub); free(sub_b);
     free(ctl); free(ctr);
     if (blur) { free(lb); free(rb); }
     free(l); free(r);
     return 0;
+}
+
+int orc_process(const uint8_t *left, const uint8_t *right,
+                const uint8_t *sky_l, const uint8_t *sky_r,
+                int h, int w, int scale, int D, int P1, int P2,
+                float uniq, float lr_dis, int blur, int views, orc_result *res)
+{
+    return process_mode(left, right, sky_l, sky_r, h, w, scale, D, P1, P2, uniq, lr_dis, blur,
+                        views, res, MODE_PARITY);
+}
+
+int orc_process_lean(const uint8_t *left, const uint8_t *right,
+                     const uint8_t *sky_l, const uint8_t *sky_r,
+                     int h, int w, int scale, int D, int P1, int P2,
+                     float uniq, float lr_dis, int blur, int views, orc_result *res)
+{
+    return process_mode(left, right, sky_l, sky_r, h, w, scale, D, P1, P2, uniq, lr_dis, blur,
+                        views, res, MODE_LEAN);
+}
+
+int orc_process_refplace(const uint8_t *left, const uint8_t *right,
+                         const uint8_t *sky_l, const uint8_t *sky_r,
+                         int h, int w, int scale, int D, int P1, int P2,
+                         float uniq, float lr_dis, int blur, int views, orc_result *res)
+{
+    return process_mode(left, right, sky_l, sky_r, h, w, scale, D, P1, P2, uniq, lr_dis, blur,
+                        views, res, MODE_REFPLACE);
 }

@@ -4,7 +4,8 @@
  * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libsgm_hip.so, the
  * stereo_matching_amd package) may link, load or call this code.  It is used
  * by tests/ as the parity checker, by __graft_entry__.smoke() as the checker,
- * and by bench.py's cpu_baseline leg as the timed CPU baseline ("kind": "port").
+ * and by bench.py's cpu_baseline leg as the timed CPU baseline ("kind": "port",
+ * orc_process_refplace: the reference's OpenMP placement).
  *
  * PARITY STATUS: "parity unpinned".  The reference (C++/OpenCV/ROS catkin
  * package) is unbuildable in this image: src/{Solver,SGM,cost}.cpp include
@@ -111,6 +112,26 @@ int orc_process(const uint8_t *left, const uint8_t *right,
                 const uint8_t *sky_l, const uint8_t *sky_r,
                 int h, int w, int scale, int D, int P1, int P2,
                 float uniq, float lr_dis, int blur, int views, orc_result *res);
+
+/* The same outputs as orc_process from 3 cost-sized volumes instead of 10
+ * (C, S = ((L1+L2)+L3)+L4, T = L5+L6; the paths stream their chain state and
+ * add in the reference's association order).  Bit-identical to orc_process;
+ * used where 10 volumes do not fit (4K256: 25.5 GB instead of 85 GB). */
+int orc_process_lean(const uint8_t *left, const uint8_t *right,
+                     const uint8_t *sky_l, const uint8_t *sky_r,
+                     int h, int w, int scale, int D, int P1, int P2,
+                     float uniq, float lr_dis, int blur, int views, orc_result *res);
+
+/* The same outputs as orc_process with the reference's OpenMP placement and
+ * memory (cost + 8 path volumes): parallel only where the reference has
+ * `omp parallel for` (census and DSI rows, L1/L2 rows, L3/L4 columns, the
+ * columns of each row of the L5/L6 and L7/L8 pair loops, sub-pixel rows, LR
+ * rows); both cost filters and the fused aggregation + WTA sequential
+ * (Solver.cpp:296-368, SGM.cpp:372-418).  bench.py's CPU baseline. */
+int orc_process_refplace(const uint8_t *left, const uint8_t *right,
+                         const uint8_t *sky_l, const uint8_t *sky_r,
+                         int h, int w, int scale, int D, int P1, int P2,
+                         float uniq, float lr_dis, int blur, int views, orc_result *res);
 
 /* Threads the OpenMP regions will use (1 if built without OpenMP). */
 int orc_max_threads(void);

@@ -28,7 +28,7 @@ SGM_VIEW_RIGHT = 1
 # Every symbol include/sgm_hip.h declares.
 EXPORTS = (
     "sgm_default_params", "sgm_create", "sgm_destroy", "sgm_last_error", "sgm_get_size",
-    "sgm_device_bytes", "sgm_process", "sgm_process_device", "sgm_post_filter_host",
+    "sgm_device_bytes", "sgm_process", "sgm_process_device",
     "sgm_post_filter_device", "sgm_stage_census", "sgm_stage_cost", "sgm_stage_path",
     "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
     "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine", "sgm_sky_detect_device",
@@ -100,7 +100,6 @@ def lib():
     L.sgm_device_bytes.restype = ctypes.c_size_t
     L.sgm_process.argtypes = [P, P, P, I, P, P, I, P, I, P]
     L.sgm_process_device.argtypes = [P, P, P, I, P, P, I, P, I, P, P]
-    L.sgm_post_filter_host.argtypes = [P, I, I, I, I]
     L.sgm_post_filter_device.argtypes = [P, P, I, P]
     L.sgm_lr_check_device.argtypes = [P, P, I, P, I, P, I, P]
     L.sgm_stage_post_filter.argtypes = [P, P]

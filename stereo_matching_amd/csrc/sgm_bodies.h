@@ -10,13 +10,12 @@
 
 namespace sgm {
 
-// Segment length K (steps between checkpoints).  The vertical family's final
-// kernel holds five K x V register arrays, so it uses a shorter K to stay at
-// <= 128 VGPRs (four waves per SIMD).
+// Segment length K (steps between checkpoints): seg_k_hd / seg_k_v
+// (sgm_internal.h), the one definition the allocation and guards share.
 template <int V>
-constexpr int pair_k() { return V >= 4 ? 8 : 16; }
+constexpr int pair_k() { return seg_k_hd(V); }
 template <int V>
-constexpr int pair_kv() { return V >= 4 ? 4 : 8; }
+constexpr int pair_kv() { return seg_k_v(V); }
 template <int FAM, int V>
 constexpr int family_k() { return FAM == PAIR_V ? pair_kv<V>() : pair_k<V>(); }
 
@@ -698,6 +697,10 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
 
     static_assert(NB == 2 || NB == 3, "producer buffers");
     static_assert(RH == 1 || RH == 2, "consumer ring halves");
+    // the final pass's WTA loads reach K-1 rows above row 0 of T: the guard
+    // allocated before T (t_guard_rows, sgm_capi.hip) must cover them
+    static_assert(MODE != PAIR_FINAL || K - 1 <= t_guard_rows(V == 4 ? 256 : (V == 2 ? 128 : 64)),
+                  "T guard rows");
     constexpr int FD = FAM == PAIR_H ? 0 : (FAM == PAIR_V ? 2 : 5);
     constexpr int BD = FAM == PAIR_H ? 1 : (FAM == PAIR_V ? 3 : 6);
     constexpr bool FINAL = MODE == PAIR_FINAL;

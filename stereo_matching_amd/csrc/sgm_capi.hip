@@ -37,8 +37,9 @@ struct sgm_handle {
     hipStream_t st;       // the handle's own stream (host API, stages)
     hipStream_t aux[1];      // right view (two-view frames)
     hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1, ev_pf;
-    hipEvent_t ev_last;   // recorded on last_st when a call comes on another stream (StreamScope)
+    hipEvent_t ev_last;   // the end of the last call's work on last_st (StreamScope)
     hipStream_t last_st;  // the stream of the last entry point's work (null: none yet)
+    bool last_recorded;   // ev_last was recorded at the end of that call (a caller's stream)
     uint8_t *d_in[2];     // full-size input staging (host API)
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
@@ -103,15 +104,30 @@ struct DeviceGuard {
 // call's work included -- and makes its own stream wait for it.  Calls on one
 // stream record nothing (an event record costs the next kernel a ~5 us
 // dispatch gap: the gap between back-to-back frames in the rocprof trace).
+// Orders calls on different streams (they share the handle's scratch).  A
+// call on a CALLER's stream records ev_last on that stream as it returns,
+// while the stream certainly exists; a call on the handle's own stream records
+// nothing (the same-stream path stays free of event records) and a later
+// call on another stream records ev_last on the handle's stream, which the
+// handle owns.  So no stream handle of the caller is kept past the call that
+// used it.  Entry points construct the scope after their argument checks, so
+// a call rejected before enqueueing anything leaves the state untouched.
 struct StreamScope {
     sgm_handle *h;
     hipStream_t st;
     StreamScope(sgm_handle *handle, void *stream)
         : h(handle), st(stream ? (hipStream_t)stream : handle->st) {
-        if (h->last_st && h->last_st != st && hipEventRecord(h->ev_last, h->last_st) == hipSuccess)
-            (void)hipStreamWaitEvent(st, h->ev_last, 0);
+        if (h->last_st && h->last_st != st) {
+            if (h->last_recorded)
+                (void)hipStreamWaitEvent(st, h->ev_last, 0);
+            else if (hipEventRecord(h->ev_last, h->last_st) == hipSuccess)
+                (void)hipStreamWaitEvent(st, h->ev_last, 0);
+        }
     }
-    ~StreamScope() { h->last_st = st; }
+    ~StreamScope() {
+        h->last_st = st;
+        h->last_recorded = st != h->st && hipEventRecord(h->ev_last, st) == hipSuccess;
+    }
 };
 
 int set_err(sgm_handle *h, int code, const char *fmt, ...) {
@@ -976,61 +992,6 @@ int sgm_get_profile(sgm_handle *h, sgm_kernel_stat *out, int max, int *count) {
     if (count) *count = out ? (n < max ? n : max) : n;
     for (auto &st : h->stats) { st.launches = 0; st.total_ms = 0; }
     for (auto &e : h->stat_elems) e = 0.0;
-    return SGM_OK;
-}
-
-// ----------------------------------------------------------- post filter
-
-namespace {
-int uf_find(std::vector<int> &p, int i) {
-    while (p[i] != i) {
-        p[i] = p[p[i]];
-        i = p[i];
-    }
-    return i;
-}
-}  // namespace
-
-int sgm_post_filter_host(float *F, int H, int W, int D, int scale) {
-    if (!F || H <= 0 || W <= 0 || D <= 0 || scale <= 0) return SGM_ERR_INVALID_ARG;
-    // Median fill, Solver.cpp:604-630: sequential, row-major, in place,
-    // int-truncated samples, more than 12 valid samples required.
-    int v[25];
-    for (int i = 2; i < H - 2; ++i)
-        for (int j = 2; j < W - 2; ++j) {
-            if (F[(size_t)i * W + j] <= D - 1) continue;
-            int cnt = 0;
-            for (int m = i - 2; m <= i + 2; ++m)
-                for (int n = j - 2; n <= j + 2; ++n) {
-                    const float x = F[(size_t)m * W + n];
-                    if (x <= D - 1) v[cnt++] = (int)x;
-                }
-            if (cnt > 12) {
-                std::sort(v, v + cnt);
-                F[(size_t)i * W + j] = (float)v[cnt / 2];
-            }
-        }
-    // Speckle removal, Solver.cpp:514-566 (single-thread semantics): 4-connected
-    // components of |a-b| < 2 with at most 1000/scale pixels become invalid.
-    const size_t n = (size_t)H * W;
-    std::vector<int> parent(n), area(n, 0);
-    for (size_t k = 0; k < n; ++k) parent[k] = (int)k;
-    for (int i = 0; i < H; ++i)
-        for (int j = 0; j < W; ++j) {
-            const size_t k = (size_t)i * W + j;
-            if (j + 1 < W && fabsf(F[k] - F[k + 1]) < 2) {
-                int a = uf_find(parent, (int)k), b = uf_find(parent, (int)k + 1);
-                if (a != b) parent[a] = b;
-            }
-            if (i + 1 < H && fabsf(F[k] - F[k + W]) < 2) {
-                int a = uf_find(parent, (int)k), b = uf_find(parent, (int)(k + W));
-                if (a != b) parent[a] = b;
-            }
-        }
-    for (size_t k = 0; k < n; ++k) area[uf_find(parent, (int)k)]++;
-    const int max_size = 1000 / scale;
-    for (size_t k = 0; k < n; ++k)
-        if (area[uf_find(parent, (int)k)] <= max_size) F[k] = (float)(D + 1);
     return SGM_OK;
 }
 

@@ -12,10 +12,22 @@ namespace sgm {
 // read up to 64 positions (x D <= 256) past the last row's end.
 constexpr size_t kVolGuard = 64 * 256 + 256;
 
+// Disparities per lane of a wave64 chain (lane l holds d = l*V .. l*V+V-1).
+constexpr int vals_per_lane(int D) { return D >= 256 ? 4 : (D >= 128 ? 2 : 1); }
+
+// Segment lengths K (chain steps between checkpoints) of the pair families,
+// by values per lane.  The one definition: the kernels' pair_k<V>() /
+// pair_kv<V>() (sgm_bodies.h), the checkpoint allocation (pair_ckpt_floats)
+// and the guard below all derive from these.  The vertical family's final
+// kernel holds five K x V register arrays, so it uses a shorter K to stay at
+// <= 128 VGPRs (four waves per SIMD).
+constexpr int seg_k_hd(int V) { return V >= 4 ? 8 : 16; }   // PAIR_H, PAIR_D2
+constexpr int seg_k_v(int V) { return V >= 4 ? 4 : 8; }     // PAIR_V
+
 // Rows of slack before the T volume read by the final pass (pair_split_body's
 // WTA waves load a chunk from its top row; the partial last chunk's top lies
 // up to K-1 rows above row 0, K = the vertical family's segment length).
-constexpr int t_guard_rows(int D) { return (D >= 256 ? 4 : 8) - 1; }
+constexpr int t_guard_rows(int D) { return seg_k_v(vals_per_lane(D)) - 1; }
 
 // Geometry of one frame on the working (decimated) grid.
 struct Geom {

@@ -19,13 +19,12 @@
 namespace sgm {
 
 
-static inline int vals_per_lane(int D) { return D >= 256 ? 4 : (D >= 128 ? 2 : 1); }
 static inline int chain_len(int family, Geom g) { return family == PAIR_H ? g.W : g.H; }
 static inline int num_chains(int family, Geom g) { return family == PAIR_H ? g.H : g.W; }
 
 size_t pair_ckpt_floats(int family, Geom g) {
     const int V = vals_per_lane(g.D);
-    const int K = family == PAIR_V ? (V >= 4 ? 4 : 8) : (V >= 4 ? 8 : 16);
+    const int K = family == PAIR_V ? seg_k_v(V) : seg_k_hd(V);
     const int n = chain_len(family, g);
     const size_t nseg = (size_t)((n + K - 1) / K);
     return (size_t)num_chains(family, g) * nseg * g.D;

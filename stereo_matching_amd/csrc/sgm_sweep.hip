@@ -117,7 +117,11 @@ hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream
 // ------------------------------------------------------------- LR check
 
 // SGM.cpp:803-818: dr = FR[i][(int)(j - dl/s)] when j >= dl; invalid if
-// |dl - dr| > LR_CHECK_DIS.  Pitches in floats; out may alias fl.
+// |dl - dr| > LR_CHECK_DIS.  Pitches in floats; out may alias fl.  The column
+// is clamped to the row before the int conversion (as oracle/sgm_oracle.c's
+// orc_lr_check): a no-op for every map compute_subpixel produces (dl >= 0 or
+// NaN, so 0 <= j - dl/s <= j; DESIGN.md "LR check domain"); for arbitrary maps
+// passed to sgm_lr_check_device the reference would read another row.
 __global__ __launch_bounds__(256) void lr_kernel(const float *fl, int fl_pitch,
                                                  const float *__restrict__ fr, int fr_pitch,
                                                  float *out, int out_pitch, int H, int W, int D,
@@ -125,8 +129,12 @@ __global__ __launch_bounds__(256) void lr_kernel(const float *fl, int fl_pitch,
     const int j = bid_x() * 256 + tid_x(), i = bid_y();
     if (j >= W) return;
     float dl = fl[(size_t)i * fl_pitch + j];
-    if (j >= dl) {
-        const int jr = clampi((int)(j - dl / scale), 0, W - 1);
+    // j >= NaN is false (IEEE); tested on the bits: the library builds with
+    // -fno-honor-nans, under which the compiler may assume dl is not NaN
+    const bool nan = (__float_as_uint(dl) & 0x7fffffffu) > 0x7f800000u;
+    if (!nan && j >= dl) {
+        const float x = j - dl / scale;
+        const int jr = x < 0.f ? 0 : (x > (float)(W - 1) ? W - 1 : (int)x);
         const float dr = fr[(size_t)i * fr_pitch + jr];
         if (fabsf(dl - dr) > lr) dl = (float)(D + 1);
     }

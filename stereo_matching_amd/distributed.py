@@ -51,27 +51,53 @@ def gather_maps(local: torch.Tensor, n_items: int, group=None) -> torch.Tensor |
     return out
 
 
+def comm_device(group=None) -> torch.device:
+    """Where a collective's buffers live: the current HIP device for RCCL
+    (backend "nccl"), the host for gloo (which this module stages through)."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], map_shape,
-                  *, dtype=torch.float32, device="cpu", group=None):
+                  *, dtype=torch.float32, device=None, group=None):
     """Runs `compute(pair) -> H x W map` on this rank's shard of `pairs` and
     gathers the maps to rank 0 (returned there, None elsewhere).
 
-    `map_shape` (H, W), `dtype` and `device` describe the maps `compute`
-    returns (for an SGM handle: (rows, cols), float32, its cuda device): a
-    rank whose shard is empty (fewer pairs than ranks) sends a zero stack of
-    that kind without computing a frame, so the gather's buffers agree on
-    every rank (RCCL needs them on the GPU, gloo on the host)."""
+    `map_shape` (H, W) and `dtype` describe the maps `compute` returns (for an
+    SGM handle: (rows, cols), float32).  The gather runs where the process
+    group's backend needs its buffers (`device`, default `comm_device()`: the
+    current GPU for RCCL, the host for gloo, so HIP maps are staged through
+    host memory there); the batch comes back on that device.  A rank whose
+    shard is empty (fewer pairs than ranks) sends a zero stack without
+    computing a frame, so the gather's buffers agree on every rank.
+
+    Failures are agreed on before any gather: if `compute` raises or returns
+    a map of the wrong shape on any rank, every rank raises (a rank that
+    raised alone would leave the others blocked in the gather)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     h, w = map_shape
-    mine = [compute(pairs[i]) for i in shard(len(pairs), rank, world)]
-    for m in mine:
-        if tuple(m.shape) != (h, w):
-            raise ValueError(f"compute returned a {tuple(m.shape)} map, expected {(h, w)}")
+    dev = torch.device(device) if device is not None else comm_device(group)
+    mine, err = [], None
+    try:
+        for i in shard(len(pairs), rank, world):
+            m = compute(pairs[i])
+            if tuple(m.shape) != (h, w):
+                raise ValueError(f"compute returned a {tuple(m.shape)} map, expected {(h, w)}")
+            mine.append(m)
+    except Exception as e:  # noqa: BLE001 -- re-raised below, on every rank
+        err = e
+    flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=comm_device(group))
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if err is not None:
+        raise err
+    if int(flag.item()):
+        raise RuntimeError("process_batch: compute failed on another rank")
     if mine:
-        local = torch.stack([m.to(device=device, dtype=dtype) for m in mine])
+        local = torch.stack([m.to(device=dev, dtype=dtype) for m in mine])
     else:
-        local = torch.empty((0, h, w), dtype=dtype, device=device)
+        local = torch.empty((0, h, w), dtype=dtype, device=dev)
     return gather_maps(local, len(pairs), group)
 
 
@@ -82,15 +108,24 @@ class PipelinedGather:
     map (RCCL over xGMI: its stream waits for the map's producer, nothing
     waits for it); a buffer's previous gather is only waited for when the
     buffer comes round again, and `drain()` waits for all of them.  With
-    depth 2 the gather of step k runs under the kernels of step k+1."""
+    depth 2 the gather of step k runs under the kernels of step k+1.
+
+    With gloo and device maps (tests: several ranks sharing one GPU) each
+    submit first copies the map to a host buffer (a synchronous copy, so the
+    map's producer has finished) and gathers that; `gathered()` then returns
+    host tensors."""
 
     def __init__(self, shape, dtype, device, depth: int = 2, group=None):
         self.group = group
         self.depth = depth
         world = dist.get_world_size(group)
         self.root = dist.get_rank(group) == 0
+        device = torch.device(device)
         self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(depth)]
-        self.recv = [[torch.empty(shape, dtype=dtype, device=device) for _ in range(world)]
+        self.staged = dist.get_backend(group) != "nccl" and device.type != "cpu"
+        cdev = torch.device("cpu") if self.staged else device
+        self.host = [torch.empty(shape, dtype=dtype) for _ in range(depth)] if self.staged else None
+        self.recv = [[torch.empty(shape, dtype=dtype, device=cdev) for _ in range(world)]
                      if self.root else None for _ in range(depth)]
         self.work = [None] * depth
         self.k = 0
@@ -104,7 +139,11 @@ class PipelinedGather:
 
     def submit(self) -> None:
         i = self.k % self.depth
-        self.work[i] = dist.gather(self.bufs[i], gather_list=self.recv[i], dst=0, group=self.group,
+        send = self.bufs[i]
+        if self.staged:
+            self.host[i].copy_(send)
+            send = self.host[i]
+        self.work[i] = dist.gather(send, gather_list=self.recv[i], dst=0, group=self.group,
                                    async_op=True)
         self.k += 1
 

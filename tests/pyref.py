@@ -208,7 +208,10 @@ def lr_check(FL, FR, D, scale=1, lr_dis=1.0):
         for j in range(W):
             dl = FL[i, j]
             if f32(j) >= dl:
-                jr = int(f32(j) - dl / f32(scale))
+                # clamped column (the build's choice where SGM.cpp:812 would read
+                # outside the row; never acts on maps compute_subpixel produces)
+                x = f32(j) - dl / f32(scale)
+                jr = 0 if x < 0 else (W - 1 if x > W - 1 else int(x))
                 if abs(dl - FR[i, jr]) > f32(lr_dis):
                     FL[i, j] = D + 1
     return FL

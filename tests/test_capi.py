@@ -104,7 +104,6 @@ def test_null_arguments_rejected(lib):
     assert lib.sgm_destroy(None) == _capi.SGM_ERR_INVALID_ARG
     assert lib.sgm_process(None, None, None, 0, None, None, 0, None, 0, None) == \
         _capi.SGM_ERR_INVALID_ARG
-    assert lib.sgm_post_filter_host(None, 1, 1, 32, 1) == _capi.SGM_ERR_INVALID_ARG
 
 
 def test_no_silent_fallback_without_gpu(lib):

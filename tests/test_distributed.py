@@ -187,3 +187,44 @@ def test_view_split_world4_gloo():
     for team in range(2):
         ref = oracle.process(*synthetic.stereo_pair(H, W, D, team), D)
         assert np.array_equal(res[2 * team].view(np.uint32), ref["lr"].view(np.uint32)), team
+
+
+def _bad_compute(pair):
+    # rank 1's pairs come back with the wrong shape
+    m = _compute(pair)
+    return m[:-1] if dist.get_rank() == 1 else m
+
+
+def _err_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            distributed.process_batch(_pairs(4), _bad_compute, (H, W))
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, f"ValueError: {e}"))
+        except RuntimeError as e:
+            q.put((rank, f"RuntimeError: {e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_process_batch_error_reaches_every_rank():
+    # a bad map on one rank must not leave the others blocked in
+    # the gather -- the ranks agree on the failure first and all raise
+    import oracle
+    oracle.build()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_err_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1].startswith("ValueError") and "expected" in res[1]
+    assert res[0].startswith("RuntimeError") and "another rank" in res[0]
+

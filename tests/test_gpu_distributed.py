@@ -1,0 +1,171 @@
+"""The multi-GPU driver (stereo_matching_amd/distributed.py)
+carrying HIP-computed disparity maps, on the one-GPU box:
+
+* world 1 on the nccl backend (RCCL): process_batch with an SGM handle
+  computing device maps, and PipelinedGather over 6 steps (bench.py's
+  overlapped per-step gather) -- the code config 4 runs on 8 GPUs;
+* two gloo ranks sharing cuda:0 with CUDA maps: process_batch over an uneven
+  batch (maps staged through the host) and the staged PipelinedGather;
+* bench.py itself under torch.distributed.run (world 1, nccl).
+
+Every gathered map must equal the map a single handle computes for that pair,
+bit for bit.  Each case runs in fresh child processes (torch's HIP runtime
+initialises before the library's, as in bench.py)."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+COMMON = r"""
+import os, sys, numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from stereo_matching_amd import SGM, synthetic
+from stereo_matching_amd import distributed as sd
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+H, W, D = 375, 1242, 128
+PAIRS = [synthetic.stereo_pair(H, W, D, pair_index=i) for i in range(5)]
+
+def single(pair):
+    # the reference map: one handle, one pair, device in / device out
+    with SGM(H, W, 1, D, device=0) as s:
+        out = torch.empty((H, W), dtype=torch.float32, device=dev)
+        l, r = (torch.from_numpy(a).to(dev) for a in pair)
+        s.process_device(l.data_ptr(), r.data_ptr(), out.data_ptr(),
+                         stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        return out.cpu()
+
+def same(a, b):
+    return torch.equal(a.cpu().contiguous().view(torch.int32), b.cpu().contiguous().view(torch.int32))
+
+sgm = SGM(H, W, 1, D, device=0)
+stream = torch.cuda.current_stream(dev)
+def compute(pair):
+    l, r = (torch.from_numpy(a).to(dev) for a in pair)
+    out = torch.empty((H, W), dtype=torch.float32, device=dev)
+    sgm.process_device(l.data_ptr(), r.data_ptr(), out.data_ptr(), stream=stream.cuda_stream)
+    return out
+"""
+
+WORLD1_NCCL = COMMON + r"""
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+assert dist.get_backend() == "nccl"
+want = [single(p) for p in PAIRS]
+batch = sd.process_batch(PAIRS, compute, (H, W))
+assert batch.is_cuda and tuple(batch.shape) == (5, H, W)
+for k in range(5):
+    assert same(batch[k], want[k]), k
+print("process_batch ok", flush=True)
+# bench.py's overlapped gather: step k writes buffer k % 2 while step k-1's
+# gather may still run; each step's gathered map must be that step's pair
+pipe = sd.PipelinedGather((H, W), torch.float32, dev, depth=2)
+dl = [torch.from_numpy(p[0]).to(dev) for p in PAIRS]
+dr = [torch.from_numpy(p[1]).to(dev) for p in PAIRS]
+for k in range(6):
+    buf = pipe.buffer()
+    if k >= 2:
+        assert same(pipe.gathered(k - 2)[0], want[(k - 2) % 5]), k - 2
+    sgm.process_device(dl[k % 5].data_ptr(), dr[k % 5].data_ptr(), buf.data_ptr(),
+                       stream=stream.cuda_stream)
+    pipe.submit()
+pipe.drain()
+for k in (4, 5):
+    assert same(pipe.gathered(k)[0], want[k % 5]), k
+print("pipelined gather ok", flush=True)
+sgm.close()
+dist.destroy_process_group()
+print("world1 nccl ok")
+"""
+
+GLOO2 = COMMON + r"""
+rank = int(sys.argv[3])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=rank,
+                        world_size=2)
+pairs = PAIRS[:3]                       # uneven: rank 0 holds pairs 0, 2; rank 1 pair 1
+batch = sd.process_batch(pairs, compute, (H, W))
+pipe = sd.PipelinedGather((H, W), torch.float32, dev, depth=2)
+seen = {}
+for k in range(4):
+    buf = pipe.buffer()
+    if k >= 2 and rank == 0:
+        seen[k - 2] = [t.clone() for t in pipe.gathered(k - 2)]
+    p = PAIRS[(2 * k + rank) % 5]       # rank r's pair of step k
+    l, r = (torch.from_numpy(a).to(dev) for a in p)
+    sgm.process_device(l.data_ptr(), r.data_ptr(), buf.data_ptr(), stream=stream.cuda_stream)
+    pipe.submit()
+pipe.drain()
+if rank == 0:
+    for k in (2, 3):
+        seen[k] = [t.clone() for t in pipe.gathered(k)]
+    assert batch.device.type == "cpu" and tuple(batch.shape) == (3, H, W)
+    for k in range(3):
+        assert same(batch[k], single(pairs[k])), ("batch", k)
+    for k in range(4):
+        for r in range(2):
+            assert same(seen[k][r], single(PAIRS[(2 * k + r) % 5])), ("pipe", k, r)
+    print("gloo2 ok", flush=True)
+else:
+    assert batch is None
+sgm.close()
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def _port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return str(sk.getsockname()[1])
+
+
+@pytest.mark.timeout(300)
+def test_world1_nccl_process_batch_and_pipelined_gather():
+    r = subprocess.run([sys.executable, "-c", WORLD1_NCCL, ROOT, _port()], capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "world1 nccl ok" in r.stdout, r.stdout[-3000:] + r.stderr[-4000:]
+
+
+@pytest.mark.timeout(300)
+def test_two_gloo_ranks_on_one_gpu():
+    port = _port()
+    procs = [subprocess.Popen([sys.executable, "-c", GLOO2, ROOT, port, str(rank)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for rank in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, (so, se) in zip(procs, outs):
+        assert p.returncode == 0, so[-2000:] + se[-4000:]
+    assert "gloo2 ok" in outs[0][0]
+
+
+@pytest.mark.timeout(300)
+def test_bench_under_torch_distributed_run():
+    # the driver's multi-GPU launch line at N = 1: process group on nccl
+    # (RCCL), the pipelined gather of every step's map inside the timed region
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", _port(), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "4", "--warmup", "2", "--no-profile-pass"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
+    assert "RCCL" in rec["config"]["parallelism"]
+    assert rec["cpu_baseline"] is not None

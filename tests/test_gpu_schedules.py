@@ -57,10 +57,26 @@ def test_joint_cost_launch_matches_per_view(h, w, D, sky_l, sky_r):
 
 def test_joint_final_matches_per_view():
     # 512 x 1056 x 128 f32 = 277 MB per volume: above the Infinity Cache, so
-    # the default schedule runs both final passes as one launch
+    # the whole-volume schedule (SGM_BAND_ROWS=0: pair_final2_kernel is the
+    # unbanded schedule's joint final launch) runs both final passes as one
+    # launch; SGM_SPLIT_FINAL=1 runs one per view
     h, w, D = 512, 1056, 128
     assert h * w * D * 4 > 256 * 1024 * 1024
-    _same(_run(h, w, D, False, False, {}), _run(h, w, D, False, False, {"SGM_SPLIT_FINAL": "1"}))
+    _same(_run(h, w, D, False, False, {"SGM_BAND_ROWS": "0"}),
+          _run(h, w, D, False, False, {"SGM_BAND_ROWS": "0", "SGM_SPLIT_FINAL": "1"}))
+
+
+@pytest.mark.parametrize("band_rows", ["16", "0"])
+def test_banded_concurrent_views_match_default(band_rows):
+    # SGM_CONCURRENT_VIEWS=1 on a banded frame: each view runs its forward
+    # bands, its own H pair and its backward bands on its own stream with
+    # per-view carries (run_frame's split_h = false path); against the
+    # default single-stream schedule of the same bands
+    h, w, D = 200, 640, 128
+    env = {"SGM_BAND_ROWS": band_rows}
+    _same(_run(h, w, D, True, True, env), _run(h, w, D, True, True, dict(env, SGM_CONCURRENT_VIEWS="1")))
+    _same(_run(h, w, D, False, True, env),
+          _run(h, w, D, False, True, dict(env, SGM_CONCURRENT_VIEWS="1", SGM_FWD_BANDS="0")))
 
 
 CROSS_STREAM = r"""

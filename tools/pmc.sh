@@ -2,7 +2,7 @@
 # HBM-side traffic per kernel from PMC counters (MI355X_MICROARCH.md "HBM"):
 # one rocprofv3 pass per counter, kernel trace only, then tools/pmc_reduce.py
 # writes per-launch bytes to profiles/pmc_traffic.json.
-# Usage (GPU box): bash tools/pmc.sh TAG [config]
+# Usage (GPU box): GIT_SHA=<commit> bash tools/pmc.sh TAG [config]
 set -o pipefail
 TAG=${1:-dev}
 CFG=${2:-k128}

@@ -76,9 +76,17 @@ def main():
         data = json.load(open(path))
     data[cfg] = {k: v["bytes"] for k, v in out.items()}
     data.setdefault("_detail", {})[cfg] = out
-    data.setdefault("_tags", {})[cfg] = tag
-    data["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (run tag per "
-                       "config in _tags); FETCH_SIZE doubled (gfx950), KiB -> bytes; per-launch means")
+    sys.path.insert(0, ROOT)
+    from bench import source_sha
+    # the run tag, the commit the tree was taken from (GIT_SHA, passed in by
+    # the caller: the GPU box has no .git) and the hash of the library's
+    # sources, which bench.py compares with the code it runs
+    data.setdefault("_tags", {})[cfg] = {"tag": tag, "git": os.environ.get("GIT_SHA", "unknown"),
+                                         "src_sha": source_sha()}
+    data["_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (per config in "
+                       "_tags: run tag, git commit, sha of the library sources); FETCH_SIZE "
+                       "doubled (gfx950), KiB -> bytes; per-launch means; memory-side bytes "
+                       "(Infinity Cache hits included, MI355X_MICROARCH.md 'HBM')")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
     for k, v in out.items():
