@@ -225,7 +225,11 @@ def main():
     else:
         sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter,
                   lk_refine=args.lk_refine, sky_detect=args.sky_detect)
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream for everything a step enqueues (the library's
+    # kernels, torch's copies, RCCL's stream dependencies)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     def step():
         if team:

@@ -19,6 +19,10 @@
  * frame at a time, like the reference object, Solver.h:29-30).  Use one
  * handle per device/thread.
  *
+ * Stream arguments: NULL = the handle's own stream, created non-blocking (so
+ * NOT ordered with the legacy default stream); hipStreamLegacy ((void *)1)
+ * = the legacy default stream; otherwise a hipStream_t.
+ *
  * Streams: every call on a handle uses the handle's device scratch (cost
  * volumes, checkpoints, post-filter and LKRefine buffers), so the library
  * orders calls made on different streams: a call whose stream differs from

@@ -18,6 +18,21 @@ def _ptr(a):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
+# hipStreamLegacy (hip_runtime_api.h): the legacy default ("null") stream
+_HIP_STREAM_LEGACY = 1
+
+
+def _stream(stream):
+    """The hipStream_t the C-ABI gets: None -> NULL, the handle's own stream
+    (non-blocking: NOT ordered with the null stream); 0 -> hipStreamLegacy,
+    the legacy default stream (torch's default stream reports cuda_stream 0,
+    so passing torch.cuda.current_stream().cuda_stream orders the call with
+    torch's work either way); anything else is a hipStream_t handle."""
+    if stream is None:
+        return ctypes.c_void_p(None)
+    return ctypes.c_void_p(_HIP_STREAM_LEGACY if stream == 0 else stream)
+
+
 def _u8(a, shape, what):
     a = np.ascontiguousarray(a, dtype=np.uint8)
     if a.shape != shape:
@@ -120,13 +135,15 @@ class SGM:
 
     def process_device(self, d_left: int, d_right: int, d_out: int, *, pitch: int | None = None,
                        d_sky_l: int = 0, d_sky_r: int = 0, sky_pitch: int | None = None,
-                       out_pitch: int | None = None, d_raw: int = 0, stream: int = 0) -> None:
-        """Device-pointer variant (sgm_process_device): enqueue on `stream`."""
+                       out_pitch: int | None = None, d_raw: int = 0, stream: int | None = None) -> None:
+        """Device-pointer variant (sgm_process_device): enqueue on `stream`
+        (None: the handle's own stream; a torch stream's `cuda_stream`,
+        including 0 for torch's default stream: that stream)."""
         check(self._lib.sgm_process_device(
             self._h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), pitch or self.w,
             ctypes.c_void_p(d_sky_l or None), ctypes.c_void_p(d_sky_r or None),
             sky_pitch or self.cols, ctypes.c_void_p(d_out), out_pitch or self.cols,
-            ctypes.c_void_p(d_raw or None), ctypes.c_void_p(stream or None)), self._h)
+            ctypes.c_void_p(d_raw or None), _stream(stream)), self._h)
 
     def get_disp(self) -> np.ndarray:
         """Post-filtered disparity (inc/Solver.h:36: filtered_disp after
@@ -143,14 +160,14 @@ class SGM:
 
     def lr_check_device(self, d_fl: int, d_fr: int, d_out: int, *, fl_pitch: int | None = None,
                         fr_pitch: int | None = None, out_pitch: int | None = None,
-                        stream: int = 0) -> None:
+                        stream: int | None = None) -> None:
         """The LR check (SGM.cpp:803-818) of two device sub-pixel maps, e.g.
         the left and right views computed on two GPUs (sgm_lr_check_device);
         d_out may be d_fl."""
         check(self._lib.sgm_lr_check_device(
             self._h, ctypes.c_void_p(d_fl), fl_pitch or self.cols, ctypes.c_void_p(d_fr),
             fr_pitch or self.cols, ctypes.c_void_p(d_out), out_pitch or self.cols,
-            ctypes.c_void_p(stream or None)), self._h)
+            _stream(stream)), self._h)
 
     def post_filter(self, disp) -> np.ndarray:
         """post_filter() (Solver.cpp:600-649) of a rows x cols map on the GPU
@@ -161,11 +178,11 @@ class SGM:
         check(self._lib.sgm_stage_post_filter(self._h, _ptr(f)), self._h)
         return f
 
-    def post_filter_device(self, d_disp: int, *, pitch: int | None = None, stream: int = 0) -> None:
+    def post_filter_device(self, d_disp: int, *, pitch: int | None = None, stream: int | None = None) -> None:
         """In place on a device map (sgm_post_filter_device)."""
         check(self._lib.sgm_post_filter_device(self._h, ctypes.c_void_p(d_disp),
                                                pitch or self.cols,
-                                               ctypes.c_void_p(stream or None)), self._h)
+                                               _stream(stream)), self._h)
 
     def lk_refine(self, img_l, img_r, disp) -> np.ndarray:
         """LKSubPixel::LKRefine(img_l, img_r, disp_float) (LKSubPixelImpl.cpp:
@@ -180,11 +197,11 @@ class SGM:
         return f
 
     def lk_refine_device(self, d_left: int, d_right: int, d_disp: int, *, pitch: int | None = None,
-                         disp_pitch: int | None = None, stream: int = 0) -> None:
+                         disp_pitch: int | None = None, stream: int | None = None) -> None:
         """In place on a device map (sgm_lk_refine_device)."""
         check(self._lib.sgm_lk_refine_device(
             self._h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), pitch or self.w,
-            ctypes.c_void_p(d_disp), disp_pitch or self.cols, ctypes.c_void_p(stream or None)),
+            ctypes.c_void_p(d_disp), disp_pitch or self.cols, _stream(stream)),
             self._h)
 
     def sky_detect(self, img) -> np.ndarray:
@@ -196,10 +213,10 @@ class SGM:
         return mask
 
     def sky_detect_device(self, d_img: int, d_mask: int, *, pitch: int | None = None,
-                          mask_pitch: int | None = None, stream: int = 0) -> None:
+                          mask_pitch: int | None = None, stream: int | None = None) -> None:
         check(self._lib.sgm_sky_detect_device(self._h, ctypes.c_void_p(d_img), pitch or self.w,
                                               ctypes.c_void_p(d_mask), mask_pitch or self.cols,
-                                              ctypes.c_void_p(stream or None)), self._h)
+                                              _stream(stream)), self._h)
 
     def colormap(self, disp) -> np.ndarray:
         """Solver::colormap (Solver.cpp:652-707) on the GPU: rows x cols x 3 BGR."""
