@@ -56,6 +56,8 @@ struct sgm_handle {
     float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
     int band_rows;        // rows per band of the backward phase (0: whole volume)
     bool fwd_bands;       // frames also run vfwd and stage A's diagonal roles in bands
+    bool t56;             // SGM_T56=1 (banded frames): T56 = L5 + L6 in the forward bands,
+                          // L7 as a plain sweep in the backward bands (DESIGN.md lever 2)
     int fwd_band_rows;    // rows per forward band (a multiple of 16)
     // post_filter scratch (sgm_post.hip)
     float *d_pf_orig;     // the map as it entered the median fill
@@ -397,8 +399,22 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
                    }));
             l5.band = {rb, re, h->d_carry[view][0]};
             d6.band = {rb, re, h->d_carry[view][1]};
-            HIPCHK(h, timed(h, "stage_a_d", be, st,
-                            [&] { return sgm::launch_stage_a_band(l5, d6, h->g, st); }));
+            if (h->t56) {
+                // T56 = L5 + L6 (SGM.cpp:389's first association): L5 writes T
+                // and the L6 sweep adds into it while the band is cached
+                HIPCHK(h, timed(h, "sweep_L5_init", be, st, [&] {
+                           return sgm::launch_sweep(SGM_DIR_L5, sgm::SWEEP_INIT, l5, h->g, st);
+                       }));
+                SweepArgs l6 = l5;
+                l6.acc_in = T;
+                l6.band = d6.band;
+                HIPCHK(h, timed(h, "sweep_L6_acc", be, st, [&] {
+                           return sgm::launch_sweep(SGM_DIR_L6, sgm::SWEEP_ACC, l6, h->g, st);
+                       }));
+            } else {
+                HIPCHK(h, timed(h, "stage_a_d", be, st,
+                                [&] { return sgm::launch_stage_a_band(l5, d6, h->g, st); }));
+            }
         }
         if (part == AGG_FWD) {
             hp[0] = h1;
@@ -430,8 +446,19 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
             const int ke = kb + BR < H ? kb + BR : H;
             const double be = (double)(ke - kb) / H * elems;
             d7.band = {kb, ke, h->d_carry[view][0]};
-            HIPCHK(h, timed(h, "stage_b_d2", be, st,
-                            [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
+            if (h->t56) {  // T = T56 + L7: a plain sweep, no L6 recompute
+                SweepArgs l7 = sweep_args(h);
+                l7.cost = cost;
+                l7.acc_in = T;
+                l7.acc_out = T;
+                l7.band = d7.band;
+                HIPCHK(h, timed(h, "sweep_L7_acc", be, st, [&] {
+                           return sgm::launch_sweep(SGM_DIR_L7, sgm::SWEEP_ACC, l7, h->g, st);
+                       }));
+            } else {
+                HIPCHK(h, timed(h, "stage_b_d2", be, st,
+                                [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
+            }
             l8.band = {kb, ke, h->d_carry[view][1]};
             pa.band = {kb, ke, h->d_carry[view][2]};
             HIPCHK(h, timed(h, "sweep_L8_acc", be, st,
@@ -841,6 +868,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             const char *f = getenv("SGM_FWD_BAND_ROWS");
             const int fr = f && *f ? atoi(f) / 16 * 16 : 0;
             h->fwd_band_rows = fr > 0 ? fr : h->band_rows;
+            const char *t = getenv("SGM_T56");
+            h->t56 = h->fwd_bands && t && *t == '1';
         }
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {

@@ -67,8 +67,8 @@ static void launch_sweep_v(const SweepArgs &a, Geom g, hipStream_t st) {
         }
     }
     constexpr int PF = sweep_pf<DIR>();
-    if constexpr (DIR >= 6 && MODE == SWEEP_ACC) {
-        if (a.band.ke > 0) {  // one band of the banded backward phase
+    if constexpr (DIR >= 4 && MODE != SWEEP_STORE_L) {
+        if (a.band.ke > 0) {  // one band (L7/L8: backward bands; L5/L6: forward bands)
             if (g.D == 32)
                 sweep_kernel<DIR, 1, MODE, false, PF, true><<<grid, 64, 0, st>>>(a, g);
             else if (g.D == 64)

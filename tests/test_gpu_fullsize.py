@@ -183,8 +183,8 @@ def test_4k256_schedules_agree(monkeypatch):
     left, right = synthetic.stereo_pair(h, w, D, pair_index=2)
     sky = synthetic.sky_mask(h, w)
     maps = []
-    for env in ({}, {"SGM_FWD_BANDS": "0"}, {"SGM_BAND_ROWS": "0"}):
-        for k in ("SGM_FWD_BANDS", "SGM_BAND_ROWS"):
+    for env in ({}, {"SGM_FWD_BANDS": "0"}, {"SGM_BAND_ROWS": "0"}, {"SGM_T56": "1"}):
+        for k in ("SGM_FWD_BANDS", "SGM_BAND_ROWS", "SGM_T56"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

@@ -50,15 +50,20 @@ def test_random_frame(c, split, monkeypatch):
 
 
 @pytest.mark.parametrize("c", CASES, ids=[f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_V{c['views']}" for c in CASES])
-@pytest.mark.parametrize("fwd", ["1", "0", "mixed"], ids=["fwdbands", "bwdbands", "mixed"])
+@pytest.mark.parametrize("fwd", ["1", "0", "mixed", "t56"], ids=["fwdbands", "bwdbands", "mixed", "t56"])
 def test_random_frame_banded(c, fwd, monkeypatch):
     """16-row bands (the schedule of volumes above the Infinity Cache): the
     forward phase (vfwd, L5, L6) band by band top down, both views' H pairs
     in one launch, then the backward phase (stage B's diagonal pair, L8 and
     the final pass) band by band bottom up, chain and filter states carried
-    across band edges; SGM_FWD_BANDS=0 keeps the forward phase whole, and
-    "mixed" runs 16-row forward bands with 32-row backward bands."""
+    across band edges; SGM_FWD_BANDS=0 keeps the forward phase whole,
+    "mixed" runs 16-row forward bands with 32-row backward bands, and "t56"
+    the SGM_T56 variant (L5, L6 sweeps forming T56 in the forward bands, L7 a
+    plain sweep in the backward bands)."""
     monkeypatch.setenv("SGM_BAND_ROWS", "16")
+    if fwd == "t56":  # SGM_T56: T56 = L5 + L6 in the forward bands, L7 a plain sweep
+        monkeypatch.setenv("SGM_T56", "1")
+        fwd = "1"
     if fwd == "mixed":  # forward and backward bands of different sizes
         monkeypatch.setenv("SGM_BAND_ROWS", "32")
         monkeypatch.setenv("SGM_FWD_BAND_ROWS", "16")
