@@ -102,8 +102,14 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     auto row = [&](int i, int u, bool refill) {
         float c[V];
         if (i < LAG) {
+            // row 0 stays raw; it is also what step t = 0 subtracts, kept in
+            // o1 (and so in a band's carry) rather than re-read from `in`,
+            // whose row 0 the forward bands overwrite with T (T aliases the
+            // horizontally filtered volume) before the next band starts
 #pragma unroll
             for (int v = 0; v < V; ++v) c[v] = raw0[v];
+#pragma unroll
+            for (int v = 0; v < V; ++v) o1[v] = c[v];
         } else if (i >= LAG + T) {
 #pragma unroll
             for (int v = 0; v < V; ++v) c[v] = rawl[v];
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
             if (t < T - 1) {
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
-                    const float sub = LAG == 0 ? c[v] : (t >= 1 ? o1[v] : raw0[v]);
+                    const float sub = LAG == 0 ? c[v] : o1[v];
                     sum[v] = (sum[v] + ring[u][v]) - sub;
                 }
             }
