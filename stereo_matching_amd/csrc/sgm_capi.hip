@@ -44,8 +44,9 @@ struct sgm_handle {
     uint8_t *d_sky[2];    // working-grid sky masks (host API / stages)
     uint64_t *d_ct[2];    // census words
     float *d_ch[2];       // horizontally filtered cost; reused as the T chain
-    float *d_ch_base[2];  // its allocation: d_ch is preceded by kTGuardRows rows (final pass)
+    float *d_ch_base[2];  // its allocation: d_ch is preceded by t_guard_rows rows (final pass)
     float *d_c[2];        // final cost volume
+    float *d_c_base[2];   // its allocation
     float *d_s[2];        // S chain
     uint16_t *d_disp[2];  // WTA disparity
     float *d_sub[2];      // sub-pixel disparity
@@ -166,6 +167,11 @@ bool valid_params(const sgm_params *p, char *why, size_t n) {
     const int H = p->height / p->scale, W = p->width / p->scale;
     if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
     if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
+    // SGM.cpp:374-408 keeps the previous pixel's sec_min_d when a pixel has no
+    // second distinct cost; that stale index can decide a pixel only when
+    // min/FLT_MAX > UNIQUE_RATIO, i.e. for a negative ratio, which this build
+    // therefore rejects (its WTA keeps no state across pixels)
+    if (!(p->uniqueness >= 0.0f)) { snprintf(why, n, "uniqueness must be >= 0"); return false; }
     if (p->view != SGM_VIEW_LEFT && p->view != SGM_VIEW_RIGHT) {
         snprintf(why, n, "view must be SGM_VIEW_LEFT or SGM_VIEW_RIGHT");
         return false;
@@ -203,7 +209,7 @@ int dalloc(sgm_handle *h, T **p, size_t count) {
 void free_all(sgm_handle *h) {
     for (int v = 0; v < 2; ++v) {
         (void)hipFree(h->d_in[v]); (void)hipFree(h->d_sky[v]); (void)hipFree(h->d_ct[v]);
-        (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
+        (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c_base[v]); (void)hipFree(h->d_s[v]);
         for (auto &c : h->d_carry[v]) (void)hipFree(c);
         (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
     }
@@ -356,6 +362,11 @@ int band_rows_for(Geom g) {
 // arguments in hp[0..1] (the caller launches both views' H pairs at once);
 // AGG_BWD then runs the rest.
 enum AggPart { AGG_ALL = 0, AGG_FWD = 1, AGG_BWD = 2 };
+// the view's final cost volume C and its T chain (T reuses the horizontally
+// filtered volume, dead once vfwd has read it; an in-place vfwd with T in the
+// second volume measured no faster, profiles/r03_experiments/inplace_c.txt)
+inline float *cost_buf(sgm_handle *h, int v) { return h->d_c[v]; }
+inline float *t_buf(sgm_handle *h, int v) { return h->d_ch[v]; }
 int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *T, uint16_t *disp,
                    float *sub, hipStream_t st, bool need_v_ckpt, sgm::PairArgs *defer_final = nullptr,
                    bool fwd_bands = false, int part = AGG_ALL, sgm::PairArgs *hp = nullptr) {
@@ -395,7 +406,7 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
             const double be = (double)(re - rb) / H * elems;
             va.band = {rb, re, h->d_carry[view][2]};
             HIPCHK(h, timed(h, "vfwd", be, st, [&] {
-                       return sgm::launch_vfwd(h->d_ch[view], h->d_c[view], va, h->g, st);
+                       return sgm::launch_vfwd(h->d_ch[view], cost_buf(h, view), va, h->g, st);
                    }));
             l5.band = {rb, re, h->d_carry[view][0]};
             d6.band = {rb, re, h->d_carry[view][1]};
@@ -497,7 +508,7 @@ int vfwd_view(sgm_handle *h, int view, hipStream_t st) {
     sgm::PairArgs pa = pair_args(h);
     pa.ckpt = h->d_ck[view][sgm::PAIR_V];
     HIPCHK(h, timed(h, "vfwd", elems, st, [&] {
-               return sgm::launch_vfwd(h->d_ch[view], h->d_c[view], pa, h->g, st);
+               return sgm::launch_vfwd(h->d_ch[view], cost_buf(h, view), pa, h->g, st);
            }));
     return SGM_OK;
 }
@@ -529,7 +540,7 @@ int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int p
     int rc;
     if ((rc = cost_view(h, 0, 0, d_sky_l, sky_pitch, st)) != SGM_OK) return rc;
     HIPCHK(h, timed(h, "bm_wta", elems, st, [&] {
-               return sgm::launch_bm_wta(h->d_c[0], h->p.uniqueness, h->d_disp[0], d_out, out_pitch,
+               return sgm::launch_bm_wta(cost_buf(h, 0), h->p.uniqueness, h->d_disp[0], d_out, out_pitch,
                                          g, st);
            }));
     if (d_raw)
@@ -614,7 +625,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     if (split_h) {
         sgm::PairArgs hp[2][2];
         for (int v = 0; v < 2; ++v)
-            if ((rc = aggregate_view(h, v, h->d_c[v], h->d_s[v], h->d_ch[v], h->d_disp[v],
+            if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), h->d_disp[v],
                                      v ? h->d_sub[1] : sub0, st, false, nullptr, true, AGG_FWD,
                                      hp[v])) != SGM_OK)
                 return rc;
@@ -623,11 +634,11 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                         [&] { return sgm::launch_stage_a_hpair(h1, h2, 2, g, st); }));
     }
     const int part = split_h ? AGG_BWD : AGG_ALL;
-    if ((rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], sub0, st, false,
+    if ((rc = aggregate_view(h, 0, cost_buf(h, 0), h->d_s[0], t_buf(h, 0), h->d_disp[0], sub0, st, false,
                              both_final ? &fin[0] : nullptr, fwd_bands, part)) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
-        if ((rc = aggregate_view(h, 1, h->d_c[1], h->d_s[1], h->d_ch[1], h->d_disp[1], h->d_sub[1],
+        if ((rc = aggregate_view(h, 1, cost_buf(h, 1), h->d_s[1], t_buf(h, 1), h->d_disp[1], h->d_sub[1],
                                  aux1, false, both_final ? &fin[1] : nullptr, fwd_bands,
                                  part)) != SGM_OK)
             return rc;
@@ -845,12 +856,14 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         for (int v = 0; v < (p->aux_only ? 0 : h->nviews) && !rc; ++v) {
             // the final pass addresses T chunks from their top row, which for
             // the partial last chunk lies up to K-1 rows above row 0
+            // and the row-walking passes prefetch up to PF positions past the
+            // end of the last row of C (never consumed): both volumes carry
+            // both guards
             const size_t guard = (size_t)sgm::t_guard_rows(h->g.D) * h->g.W * h->g.D;
-            if ((rc = dalloc(h, &h->d_ch_base[v], nvol + guard))) break;
+            if ((rc = dalloc(h, &h->d_ch_base[v], guard + nvol + sgm::kVolGuard))) break;
             h->d_ch[v] = h->d_ch_base[v] + guard;
-            // + guard: the row-walking forward pass prefetches up to PF
-            // positions past the end of the last row (never consumed)
-            if ((rc = dalloc(h, &h->d_c[v], nvol + sgm::kVolGuard))) break;
+            if ((rc = dalloc(h, &h->d_c_base[v], guard + nvol + sgm::kVolGuard))) break;
+            h->d_c[v] = h->d_c_base[v] + guard;
             if ((rc = dalloc(h, &h->d_s[v], nvol))) break;
             if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
             if ((rc = dalloc(h, &h->d_sub[v], npx))) break;
@@ -870,6 +883,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             h->fwd_band_rows = fr > 0 ? fr : h->band_rows;
             const char *t = getenv("SGM_T56");
             h->t56 = h->fwd_bands && t && *t == '1';
+
         }
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {
@@ -1051,14 +1065,14 @@ int sgm_stage_cost(sgm_handle *h, const uint64_t *ctl, const uint64_t *ctr, cons
     if (sky) HIPCHK(h, hipMemcpyAsync(h->d_sky[0], sky, npx, hipMemcpyHostToDevice, h->st));
     HIPCHK(h, sgm::launch_cost_h(h->d_ct[0], h->d_ct[1], sky ? h->d_sky[0] : nullptr, h->g.W, view,
                                  filters & 1, h->g, h->d_ch[0], h->st));
-    if (filters & 2) {
+    const float *res = h->d_ch[0];
+    if (filters & 2) {  // the frame's own vfwd, in place when the frames run it so
         sgm::PairArgs pa = pair_args(h);
         pa.ckpt = h->d_ck[0][sgm::PAIR_V];
-        HIPCHK(h, sgm::launch_vfwd(h->d_ch[0], h->d_c[0], pa, h->g, h->st));
-    } else {
-        HIPCHK(h, sgm::launch_copy(h->d_ch[0], h->d_c[0], h->g, h->st));
+        HIPCHK(h, sgm::launch_vfwd(h->d_ch[0], cost_buf(h, 0), pa, h->g, h->st));
+        res = cost_buf(h, 0);
     }
-    HIPCHK(h, hipMemcpyAsync(cost, h->d_c[0], nvol * 4, hipMemcpyDeviceToHost, h->st));
+    HIPCHK(h, hipMemcpyAsync(cost, res, nvol * 4, hipMemcpyDeviceToHost, h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
     return SGM_OK;
 }

@@ -174,6 +174,12 @@ hipError_t launch_census(const uint8_t *src, int pitch, Geom g, int blur, uint64
 // the main loop runs blocks of COSTH_U steps with no branches, their raw
 // costs fetched one block ahead.
 constexpr int COSTH_MAX_LDS = 64 * 1024;
+
+// The horizontally filtered volume is read once, by vfwd: non-temporal stores
+// keep it from evicting the final cost C from the Infinity Cache (default-
+// policy stores: cost_h 58 -> 50 us but vfwd and stage A slower, r02 and
+// profiles/r03_experiments/inplace_c.txt).
+__device__ __forceinline__ void costh_store(float v, float *p) { __builtin_nontemporal_store(v, p); }
 constexpr int COSTH_U = 8;
 
 __host__ __device__ constexpr int costh_pad(int D, int scale) { return D / scale + 2 * COSTH_U; }
@@ -231,7 +237,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     };
 
     if (!FILTER) {
-        for (int j = 0; j < W; ++j) __builtin_nontemporal_store(raw(j), o + (size_t)j * DS);
+        for (int j = 0; j < W; ++j) costh_store(raw(j), o + (size_t)j * DS);
         return;
     }
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, U = COSTH_U;
@@ -239,7 +245,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
 #pragma unroll
-    for (int p = 0; p < LAG; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * DS);
+    for (int p = 0; p < LAG; ++p) costh_store(raw(p), o + (size_t)p * DS);
     const int T = W - 2 * HALF;
     // hist[0] is what step t subtracts: raw[t] for t < LAG, output t-LAG after
     float hist[LAG > 0 ? LAG : 1];
@@ -247,7 +253,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     for (int p = 0; p < LAG; ++p) hist[p] = raw(p);
     auto step = [&](int t, float rw) {
         const float v = div_win<WIN>(sum);
-        __builtin_nontemporal_store(v, o + (size_t)(LAG + t) * DS);
+        costh_store(v, o + (size_t)(LAG + t) * DS);
         sum += rw;
         float a;
         if constexpr (LAG == 0) {
@@ -295,8 +301,8 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
         t += U;
     }
     for (; t < T - 1; ++t) step(t, raw(WIN + t));
-    if (T >= 1) __builtin_nontemporal_store(div_win<WIN>(sum), o + (size_t)(LAG + T - 1) * DS);
-    for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * DS);
+    if (T >= 1) costh_store(div_win<WIN>(sum), o + (size_t)(LAG + T - 1) * DS);
+    for (int p = LAG + T; p < W; ++p) costh_store(raw(p), o + (size_t)p * DS);
 }
 
 template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI, int DC>
@@ -355,7 +361,7 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
         return hamming(a, b);
     };
     if (!FILTER) {
-        for (int j = 0; j < W; ++j) __builtin_nontemporal_store(raw(j), o + (size_t)j * D);
+        for (int j = 0; j < W; ++j) costh_store(raw(j), o + (size_t)j * D);
         return;
     }
     constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1;
@@ -363,12 +369,12 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
 #pragma unroll
-    for (int p = 0; p < LAG; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
+    for (int p = 0; p < LAG; ++p) costh_store(raw(p), o + (size_t)p * D);
     const int T = W - 2 * HALF;
     float o1 = 0.0f, o2 = 0.0f;
     for (int t = 0; t < T; ++t) {
         const float v = div_win<WIN>(sum);
-        __builtin_nontemporal_store(v, o + (size_t)(LAG + t) * D);
+        costh_store(v, o + (size_t)(LAG + t) * D);
         if (t == T - 1) break;
         sum += raw(WIN + t);
         float a;
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(256) void cost_h_global_kernel(const uint64_t *__re
         o2 = o1;
         o1 = v;
     }
-    for (int p = LAG + T; p < W; ++p) __builtin_nontemporal_store(raw(p), o + (size_t)p * D);
+    for (int p = LAG + T; p < W; ++p) costh_store(raw(p), o + (size_t)p * D);
 }
 
 // rows per block and LDS bytes of the staged cost_h_kernel (R = 0: the
