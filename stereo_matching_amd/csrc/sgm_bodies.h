@@ -986,6 +986,10 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
         // results of chunk c: pixel (H-1 - cK - half*KP - px, path) = the
         // wave's top pixel (px = KP-1) + (KP-1 - px) rows
         const unsigned o_off = (unsigned)((KP - 1 - px) * W);
+        // the sub-pixel map: row-major like disp, or column-major (a.sub_cm:
+        // a chunk's KP pixels are then contiguous, whole cache lines over
+        // consecutive chunks instead of one partial line per pixel)
+        const unsigned s_off = a.sub_cm ? (unsigned)(KP - 1 - px) : o_off;
         // T for chunk c+2 is issued while chunk c is consumed (3 buffers)
         auto chunk = [&](const float (&t)[QQ], float (&tn)[QQ], int c) {
             tload(tn, c + 2 < c_hi ? c + 2 : c_hi - 1);
@@ -1005,9 +1009,10 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
                 x[k] = x4.x; x[k + 1] = x4.y; x[k + 2] = x4.z; x[k + 3] = x4.w;
                 if (px < cnt) *reinterpret_cast<float4 *>(row + k) = x4;
             }
-            wta_chunk_q<V, KP, QQ>(x, F->t[c & 1] + half * KP,
-                                   (long long)(H - c * K - (half + 1) * KP) * W + path, o_off, cnt,
-                                   lane, g.D, a.uniq, a.disp, a.sub);
+            const long long row_top = H - c * K - (half + 1) * KP;
+            wta_chunk_q<V, KP, QQ>(x, F->t[c & 1] + half * KP, row_top * W + path, o_off,
+                                   a.sub_cm ? (long long)path * H + row_top : row_top * W + path,
+                                   s_off, cnt, lane, g.D, a.uniq, a.disp, a.sub);
             bar();
         };
         float t0[QQ], t1[QQ], t2[QQ];

@@ -57,6 +57,8 @@ struct sgm_handle {
     float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
     int band_rows;        // rows per band of the backward phase (0: whole volume)
     bool fwd_bands;       // frames also run vfwd and stage A's diagonal roles in bands
+    bool sub_cm;          // two-view frames: column-major sub-pixel maps + lr_cm_kernel
+                          // (SGM_SUB_CM=0: row-major maps + lr_kernel)
     bool t56;             // SGM_T56=1 (banded frames): T56 = L5 + L6 in the forward bands,
                           // L7 as a plain sweep in the backward bands (DESIGN.md lever 2)
     int fwd_band_rows;    // rows per forward band (a multiple of 16)
@@ -369,7 +371,8 @@ inline float *cost_buf(sgm_handle *h, int v) { return h->d_c[v]; }
 inline float *t_buf(sgm_handle *h, int v) { return h->d_ch[v]; }
 int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *T, uint16_t *disp,
                    float *sub, hipStream_t st, bool need_v_ckpt, sgm::PairArgs *defer_final = nullptr,
-                   bool fwd_bands = false, int part = AGG_ALL, sgm::PairArgs *hp = nullptr) {
+                   bool fwd_bands = false, int part = AGG_ALL, sgm::PairArgs *hp = nullptr,
+                   int sub_cm = 0) {
     float **ck = h->d_ck[view];
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     sgm::PairArgs pa = pair_args(h);
@@ -451,6 +454,7 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     pa.acc_in = T;
     pa.disp = disp;
     pa.sub = sub;
+    pa.sub_cm = sub_cm;
     if (BR > 0 && !defer_final) {
         // bottom band first: the backward passes walk up
         for (int kb = 0; kb < H; kb += BR) {
@@ -543,7 +547,7 @@ int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int p
                return sgm::launch_bm_wta(cost_buf(h, 0), h->p.uniqueness, h->d_disp[0], d_out, out_pitch,
                                          g, st);
            }));
-    if (d_raw)
+    if (d_raw && d_raw != h->d_disp[0])  // (the host API passes d_disp[0] itself)
         HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
                                  hipMemcpyDeviceToDevice, st));
     if (h->p.post_filter) return post_filter(h, d_out, out_pitch, st);
@@ -625,7 +629,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     if (split_h) {
         sgm::PairArgs hp[2][2];
         for (int v = 0; v < 2; ++v)
-            if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), h->d_disp[v],
+            if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), v ? nullptr : d_raw,
                                      v ? h->d_sub[1] : sub0, st, false, nullptr, true, AGG_FWD,
                                      hp[v])) != SGM_OK)
                 return rc;
@@ -634,13 +638,16 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                         [&] { return sgm::launch_stage_a_hpair(h1, h2, 2, g, st); }));
     }
     const int part = split_h ? AGG_BWD : AGG_ALL;
-    if ((rc = aggregate_view(h, 0, cost_buf(h, 0), h->d_s[0], t_buf(h, 0), h->d_disp[0], sub0, st, false,
-                             both_final ? &fin[0] : nullptr, fwd_bands, part)) != SGM_OK)
+    // two views: the final passes write column-major sub-pixel maps (whole
+    // cache lines; lr_cm_kernel reads them through LDS tiles)
+    const int cm = h->nviews == 2 && h->sub_cm ? 1 : 0;
+    if ((rc = aggregate_view(h, 0, cost_buf(h, 0), h->d_s[0], t_buf(h, 0), d_raw, sub0, st, false,
+                             both_final ? &fin[0] : nullptr, fwd_bands, part, nullptr, cm)) != SGM_OK)
         return rc;
     if (h->nviews == 2) {
-        if ((rc = aggregate_view(h, 1, cost_buf(h, 1), h->d_s[1], t_buf(h, 1), h->d_disp[1], h->d_sub[1],
+        if ((rc = aggregate_view(h, 1, cost_buf(h, 1), h->d_s[1], t_buf(h, 1), nullptr, h->d_sub[1],
                                  aux1, false, both_final ? &fin[1] : nullptr, fwd_bands,
-                                 part)) != SGM_OK)
+                                 part, nullptr, cm)) != SGM_OK)
             return rc;
         if (both_final)
             HIPCHK(h, timed(h, "pair_bwd_L4_final", 2.0 * npx * g.D, st,
@@ -650,17 +657,18 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
             HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
         }
         HIPCHK(h, timed(h, "lr", npx, st, [&] {
-                   return sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
-                                         h->p.lr_max_diff, g, st);
+                   return cm ? sgm::launch_lr_cm(h->d_sub[0], h->d_sub[1], d_out, out_pitch,
+                                                 h->p.lr_max_diff, g, st)
+                             : sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
+                                              h->p.lr_max_diff, g, st);
                }));
     } else if (!direct_out) {
         HIPCHK(h, hipMemcpy2DAsync(d_out, (size_t)out_pitch * sizeof(float), h->d_sub[0],
                                    (size_t)g.W * sizeof(float), (size_t)g.W * sizeof(float), g.H,
                                    hipMemcpyDeviceToDevice, st));
     }
-    if (d_raw)
-        HIPCHK(h, hipMemcpyAsync(d_raw, h->d_disp[0], (size_t)g.H * g.W * sizeof(uint16_t),
-                                 hipMemcpyDeviceToDevice, st));
+    // (the raw WTA map, when asked for, was written straight into d_raw by the
+    // left view's final pass; the right view's is never written)
     // with LKRefine next, the post filter's last kernel writes LKRefine's
     // input copy instead of the map (no device copy in between)
     const bool pf_to_lk = h->p.post_filter && h->p.lk_refine;
@@ -881,6 +889,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             const char *f = getenv("SGM_FWD_BAND_ROWS");
             const int fr = f && *f ? atoi(f) / 16 * 16 : 0;
             h->fwd_band_rows = fr > 0 ? fr : h->band_rows;
+            const char *cmv = getenv("SGM_SUB_CM");
+            h->sub_cm = !(cmv && *cmv == '0');
             const char *t = getenv("SGM_T56");
             h->t56 = h->fwd_bands && t && *t == '1';
 
@@ -991,7 +1001,8 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
         HIPCHK(h, hipMemcpyAsync(h->d_sky[1], psr, npx, hipMemcpyHostToDevice, h->st));
     }
     if ((rc = run_frame(h, h->d_in[0], h->d_in[1], h->p.width, sky_l ? h->d_sky[0] : nullptr,
-                        sky_r ? h->d_sky[1] : nullptr, h->g.W, h->d_out, h->g.W, nullptr, h->st)))
+                        sky_r ? h->d_sky[1] : nullptr, h->g.W, h->d_out, h->g.W,
+                        raw_disp ? h->d_disp[0] : nullptr, h->st)))
         return rc;
     HIPCHK(h, hipMemcpyAsync(pout, h->d_out, npx * sizeof(float), hipMemcpyDeviceToHost, h->st));
     if (raw_disp)

@@ -588,10 +588,13 @@ __device__ __forceinline__ int group_min_i(int x) {
 // results go to pixel pix_top + pix_off: a wave-uniform index (SGPRs) plus
 // this lane's constant offset (>= 0), so the stores need no per-lane 64-bit
 // address arithmetic.
+// sub goes to sub_top + sub_off (its own layout: column-major maps of the
+// two-view frames), disp to pix_top + pix_off (row-major).
 template <int V, int PF, int QQ>
 __device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*tb)[tbuf_stride<V>()],
-                                            long long pix_top, unsigned pix_off, int cnt, int lane,
-                                            int Dn, float uniq, uint16_t *disp, float *sub) {
+                                            long long pix_top, unsigned pix_off, long long sub_top,
+                                            unsigned sub_off, int cnt, int lane, int Dn, float uniq,
+                                            uint16_t *disp, float *sub) {
     constexpr int LPP = 64 / PF;  // lanes per pixel
     static_assert(QQ % 4 == 0 && LPP <= 32, "QQ a multiple of 4, at most 32 lanes per pixel");
     const int px = lane / LPP, q = lane - px * LPP;
@@ -635,8 +638,11 @@ __device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*
     cnt = d == -7 ? cnt : 0;       // outputs' partial-line writes cost the final pass
 #endif
     if (q == 0 && px < cnt) {
-        (disp + pix_top)[pix_off] = (uint16_t)d;
-        (sub + pix_top)[pix_off] = f;
+        // disp: only when the frame hands out its raw WTA map (else null:
+        // these one-pixel-per-row stores are partial cache lines, ~5% of the
+        // final pass at K128 for both maps, profiles/r03_experiments/final_stores.txt)
+        if (disp) (disp + pix_top)[pix_off] = (uint16_t)d;
+        (sub + sub_top)[sub_off] = f;
     }
 }
 

@@ -90,8 +90,9 @@ struct PairArgs {
     const float *s_in;
     float *out;
     float *ckpt;
-    uint16_t *disp;
-    float *sub;
+    uint16_t *disp;      // FINAL: raw WTA map, row-major (null: not wanted)
+    float *sub;          // FINAL: sub-pixel map, row-major or (sub_cm) column-major
+    int sub_cm;          // 1: sub[col * H + row] (two-view frames: lr_cm_kernel reads it)
     const float *zero;   // >= 256 zero floats: the cost of the virtual positions
                          // that align forward passes with their checkpoints
     float p1, p2, uniq;
@@ -170,5 +171,9 @@ hipError_t launch_point_cloud(const float *disp, int pitch, const uint8_t *img, 
                               int *total, Geom g, hipStream_t st);
 hipError_t launch_lr(const float *fl, int fl_pitch, const float *fr, int fr_pitch, float *out,
                      int out_pitch, float lr, Geom g, hipStream_t st);
+// the same LR check on COLUMN-major maps fl_cm, fr_cm (x[col * H + row], as
+// the two-view frame's final passes write them), row-major out
+hipError_t launch_lr_cm(const float *fl_cm, const float *fr_cm, float *out, int out_pitch, float lr,
+                        Geom g, hipStream_t st);
 
 }  // namespace sgm

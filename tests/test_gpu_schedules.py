@@ -6,7 +6,7 @@ one launch per view, and -- for volumes above the 256 MB Infinity Cache --
 both views' final passes in one launch (pair_final2_kernel) or one per view.
 SGM_CONCURRENT_VIEWS=1 (read at sgm_create) runs the right view on a second
 stream with per-view launches; SGM_SPLIT_FINAL=1 (read per frame) keeps the
-per-view final passes.  The default schedule is pinned against the oracle by
+per-view final passes; SGM_SUB_CM=0 keeps row-major sub-pixel maps.  The default schedule is pinned against the oracle by
 test_gpu_parity.py / test_gpu_fullsize.py; these tests pin the variants to it.
 """
 from __future__ import annotations
@@ -120,3 +120,12 @@ def test_calls_on_different_streams_are_ordered():
     r = subprocess.run([sys.executable, "-c", CROSS_STREAM, root], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "cross-stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("h,w,D,sky", [(120, 330, 64, False), (200, 640, 128, True),
+                                       (72, 200, 256, True), (375, 1242, 128, False)])
+def test_column_major_sub_maps_match_row_major(h, w, D, sky):
+    # two-view frames write their sub-pixel maps column-major (whole cache lines
+    # from the final pass's one-column workgroups) and lr_cm_kernel transposes
+    # through LDS; SGM_SUB_CM=0 keeps row-major maps and lr_kernel
+    _same(_run(h, w, D, sky, sky, {}), _run(h, w, D, sky, sky, {"SGM_SUB_CM": "0"}))
