@@ -151,42 +151,38 @@ hipError_t launch_lr(const float *fl, int fl_pitch, const float *fr, int fr_pitc
 // The LR check of a two-view frame on the final passes' COLUMN-major maps
 // (x[col * H + row]: whole cache lines per column chunk for the final pass's
 // one-column workgroups) with a row-major output.  A workgroup takes 64
-// columns x 32 rows: the tile of fl and the columns of fr its reads can reach
-// (j - dl/s >= j - (D+1) for every map compute_subpixel produces) are staged
-// through LDS with 128-byte column reads, then each thread checks one pixel
-// exactly as lr_kernel does; a column outside the staged range (only for maps
-// no frame produces) is read from global memory.
+// columns x 32 rows: its fl tile is staged through LDS with 128-byte column
+// reads (a transpose), then each wave checks rows of 64 consecutive pixels
+// exactly as lr_kernel does, gathering fr(i, jr) straight from the column-
+// major map: a row's 64 reads touch ~64 columns, the same lines for all 32
+// rows of the tile, so after the first row they hit the L1/L2.
 constexpr int LRT_J = 64, LRT_I = 32;
 
 __global__ __launch_bounds__(256) void lr_cm_kernel(const float *__restrict__ fl,
                                                     const float *__restrict__ fr,
                                                     float *__restrict__ out, int out_pitch, int H,
                                                     int W, int D, int scale, float lr) {
-    extern __shared__ float lrs[];
-    const int ncol = LRT_J + D + 1;
-    float *fls = lrs;                                  // [LRT_J][LRT_I + 1]
-    float *frs = lrs + LRT_J * (LRT_I + 1);            // [ncol][LRT_I + 1]
-    const int j0 = bid_x() * LRT_J, i0 = bid_y() * LRT_I, cbase = j0 - D - 1;
+    __shared__ float fls[LRT_J][LRT_I + 1];
+    const int j0 = bid_x() * LRT_J, i0 = bid_y() * LRT_I;
     const int t = tid_x();
-    for (int idx = t; idx < LRT_J * LRT_I; idx += 256) {
-        const int c = idx / LRT_I, ii = idx - c * LRT_I, j = j0 + c, i = i0 + ii;
-        fls[c * (LRT_I + 1) + ii] = (j < W && i < H) ? fl[(size_t)j * H + i] : 0.f;
-    }
-    for (int idx = t; idx < ncol * LRT_I; idx += 256) {
-        const int c = idx / LRT_I, ii = idx - c * LRT_I, j = cbase + c, i = i0 + ii;
-        frs[c * (LRT_I + 1) + ii] = (j >= 0 && j < W && i < H) ? fr[(size_t)j * H + i] : 0.f;
+#pragma unroll
+    for (int k = 0; k < LRT_J * LRT_I / 256; ++k) {
+        const int idx = t + k * 256, c = idx / LRT_I, ii = idx - c * LRT_I, j = j0 + c, i = i0 + ii;
+        fls[c][ii] = (j < W && i < H) ? fl[(size_t)j * H + i] : 0.f;
     }
     __syncthreads();
-    for (int idx = t; idx < LRT_J * LRT_I; idx += 256) {
-        const int jj = idx % LRT_J, ii = idx / LRT_J, j = j0 + jj, i = i0 + ii;
-        if (j >= W || i >= H) continue;
-        float dl = fls[jj * (LRT_I + 1) + ii];
+    const int jj = t & (LRT_J - 1), j = j0 + jj;
+    if (j >= W) return;
+#pragma unroll
+    for (int k = 0; k < LRT_I / 4; ++k) {
+        const int ii = (t >> 6) + 4 * k, i = i0 + ii;
+        if (i >= H) break;
+        float dl = fls[jj][ii];
         const bool nan = (__float_as_uint(dl) & 0x7fffffffu) > 0x7f800000u;
         if (!nan && j >= dl) {
             const float x = j - dl / scale;
             const int jr = x < 0.f ? 0 : (x > (float)(W - 1) ? W - 1 : (int)x);
-            const int c = jr - cbase;
-            const float dr = c >= 0 && c < ncol ? frs[c * (LRT_I + 1) + ii] : fr[(size_t)jr * H + i];
+            const float dr = fr[(size_t)jr * H + i];
             if (fabsf(dl - dr) > lr) dl = (float)(D + 1);
         }
         out[(size_t)i * out_pitch + j] = dl;
@@ -195,8 +191,7 @@ __global__ __launch_bounds__(256) void lr_cm_kernel(const float *__restrict__ fl
 
 hipError_t launch_lr_cm(const float *fl_cm, const float *fr_cm, float *out, int out_pitch, float lr,
                         Geom g, hipStream_t st) {
-    const size_t smem = (size_t)(LRT_J + LRT_J + g.D + 1) * (LRT_I + 1) * sizeof(float);
-    lr_cm_kernel<<<dim3((g.W + LRT_J - 1) / LRT_J, (g.H + LRT_I - 1) / LRT_I), 256, smem, st>>>(
+    lr_cm_kernel<<<dim3((g.W + LRT_J - 1) / LRT_J, (g.H + LRT_I - 1) / LRT_I), 256, 0, st>>>(
         fl_cm, fr_cm, out, out_pitch, g.H, g.W, g.D, g.scale, lr);
     return hipGetLastError();
 }
