@@ -509,4 +509,5 @@ hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st) {
     return hipGetLastError();
 }
 
+
 }  // namespace sgm

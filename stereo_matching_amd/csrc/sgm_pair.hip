@@ -32,129 +32,12 @@ size_t pair_ckpt_floats(int family, Geom g) {
 
 // ------------------------------------------------------------ kernels
 
-// cost_vertical_filter (Solver.cpp:333-368) fused with the L3 forward pass
-// (SGM.cpp:161-199): one wave per column, lane l owning the V vertical IIR
-// chains d = l*V .. l*V+V-1.  Row i of the final cost is produced, stored,
-// and fed straight into the L3 DP; L3 is checkpointed for the PAIR_V
-// backward kernel.  The raw rows the IIR adds (raw[i + WIN/2 + 1]) stream
-// through a register ring PF rows ahead.
-// BAND (the forward bands above the Infinity Cache): rows [a.band.kb,
-// a.band.ke) only, the filter's running sum, its last output and the L3 state
-// entering the band read from a.band.carry (3 D-vectors per column) and the
-// state leaving it written back there.
+// vfwd_body (sgm_bodies.h): the vertical IIR fused with the L3 forward pass,
+// one wave per column.
 template <int V, bool FULL, int WIN, int PF, bool BAND = false>
 __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
                                                   float *__restrict__ out, PairArgs a, Geom g) {
-    constexpr int K = pair_kv<V>();
-    constexpr int HALF = WIN / 2, LAG = WIN - HALF - 1, LA = HALF + 1;
-    const int lane = tid_x();
-    const float p2v = to_vgpr(a.p2);  // dp_step's P2 operand
-    const int j = bid_x();
-    const int H = g.H;
-    const size_t stride = (size_t)g.W * g.D;
-    const int e0 = lane * V;
-    const bool active = FULL || e0 < g.D;
-    const float *col = in + (size_t)j * g.D + e0;
-    float *ocol = out + (size_t)j * g.D + e0;
-    const int nseg = (H + K - 1) / K;
-    const int r0 = H - (nseg - 1) * K;
-    float *ck = a.ckpt + (size_t)j * nseg * g.D + e0;
-    const int rb = BAND ? a.band.kb : 0;
-    const int re = BAND && a.band.ke > 0 ? a.band.ke : H;
-    // checkpoints sit after rows r0-1 + mK; the first one at or after rb
-    int ck_i = rb <= r0 - 1 ? 0 : (rb - r0 + K) / K;
-    int next_ck = r0 - 1 + ck_i * K;
-    const int T = H - 2 * HALF;
-    float *cy = BAND ? a.band.carry + (size_t)j * 3 * g.D + e0 : nullptr;
-
-    float raw0[V], rawl[V], sum[V], o1[V];
-    load_v_nt<V>(raw0, col, active);
-    load_v_nt<V>(rawl, col + (size_t)(H - 1) * stride, active);  // the only row below LAG+T (WIN=3)
-    float prev[V];
-    float pmin = 0.0f;
-    if (BAND && rb > 0) {  // the filter and path state entering the band
-        load_v<V>(sum, cy, active);
-        load_v<V>(o1, cy + g.D, active);
-        load_v<V>(prev, cy + 2 * g.D, active);
-        pmin = wave_min(lane_min(prev));
-    } else {
-#pragma unroll
-        for (int v = 0; v < V; ++v) sum[v] = 0.0f;
-#pragma unroll
-        for (int k = 0; k < WIN; ++k) {
-            float r[V];
-            load_v_nt<V>(r, col + (size_t)k * stride, active);
-#pragma unroll
-            for (int v = 0; v < V; ++v) sum[v] += r[v];
-        }
-#pragma unroll
-        for (int v = 0; v < V; ++v) o1[v] = 0.0f;
-        // L = 0, minL = 0 before row 0 makes the first step yield L = C (the
-        // path start, SGM.cpp:161-170) without a per-row select (P1, P2 >= 0)
-#pragma unroll
-        for (int v = 0; v < V; ++v) prev[v] = 0.0f;
-    }
-    float ring[PF][V];
-#pragma unroll
-    for (int u = 0; u < PF; ++u)
-        load_v_nt<V>(ring[u], col + (size_t)min(rb + LA + u, H - 1) * stride, active);
-
-    auto row = [&](int i, int u, bool refill) {
-        float c[V];
-        if (i < LAG) {
-            // row 0 stays raw; it is also what step t = 0 subtracts, kept in
-            // o1 (and so in a band's carry) rather than re-read from `in`,
-            // whose row 0 the forward bands overwrite with T (T aliases the
-            // horizontally filtered volume) before the next band starts
-#pragma unroll
-            for (int v = 0; v < V; ++v) c[v] = raw0[v];
-#pragma unroll
-            for (int v = 0; v < V; ++v) o1[v] = c[v];
-        } else if (i >= LAG + T) {
-#pragma unroll
-            for (int v = 0; v < V; ++v) c[v] = rawl[v];
-        } else {
-            const int t = i - LAG;
-#pragma unroll
-            for (int v = 0; v < V; ++v) c[v] = div_win<WIN>(sum[v]);
-            if (t < T - 1) {
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    const float sub = LAG == 0 ? c[v] : o1[v];
-                    sum[v] = (sum[v] + ring[u][v]) - sub;
-                }
-            }
-#pragma unroll
-            for (int v = 0; v < V; ++v) o1[v] = c[v];
-        }
-        store_v<V>(ocol + (size_t)i * stride, c, active);
-        // L3 forward step on the freshly filtered row
-        float L[V];
-        dp_step<V>(prev, pmin, c, L, a.p1, p2v);
-        const float nmin = wave_min(lane_min(L));
-        if (i == next_ck && ck_i < nseg - 1) {
-            store_v<V>(ck + (size_t)ck_i * g.D, L, active);
-            ++ck_i;
-            next_ck += K;
-        }
-#pragma unroll
-        for (int v = 0; v < V; ++v) prev[v] = L[v];
-        pmin = nmin;
-        if (refill) load_v_nt<V>(ring[u], col + (size_t)min(i + LA + PF, H - 1) * stride, active);
-    };
-    int i0 = rb;
-    for (; i0 + PF <= re; i0 += PF) {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) row(i0 + u, u, true);
-    }
-#pragma unroll
-    for (int u = 0; u < PF; ++u)
-        if (i0 + u < re) row(i0 + u, u, false);
-    if (BAND && re < H) {  // the state leaving the band
-        store_v<V>(cy, sum, active);
-        store_v<V>(cy + g.D, o1, active);
-        store_v<V>(cy + 2 * g.D, prev, active);
-    }
+    vfwd_body<V, FULL, WIN, PF, BAND>(in, out, a, g, bid_x(), tid_x());
 }
 
 template <int FD, int V, bool FULL, int PF>
