@@ -1,0 +1,54 @@
+"""CPU checks of bench.py's bookkeeping (no GPU): the algorithmic-byte tables
+agree with DESIGN.md's schedule, the HBM-only view never exceeds the
+algorithmic one, and the source hash that ties profiles/pmc_traffic.json to
+the code is stable and covers every library source."""
+from __future__ import annotations
+
+import json
+import os
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("D", [32, 64, 128, 256])
+def test_schedule_bytes(D):
+    # 74 B/elem per view at D <= 128 for cost + aggregation
+    # (cost_h 4 + vfwd 8.5 + stage A 16.5 + stage B 20.5 + L8 12 + final 12.5)
+    total = sum(bench.bytes_per_elem(k, D) for k in
+                ("cost_h", "vfwd", "stage_a", "stage_b", "sweep_L8_acc", "pair_bwd_L4_final"))
+    ck = 4.0 / (8 if D >= 256 else 16)
+    ckv = 4.0 / (4 if D >= 256 else 8)
+    assert total == pytest.approx(4 + (8 + ckv) + (16 + 2 * ck) + (20 + 2 * ck) + 12 + (12 + ckv))
+    if D <= 128:
+        assert total == pytest.approx(74.0)
+
+
+def test_c_reads_within_algorithmic_bytes():
+    for k in ("stage_a", "stage_b", "pair_bwd_L4_final", "sweep_L8_acc", "stage_a_hp",
+              "stage_b_d2", "stage_a_d", "stage_a_h"):
+        for D in (64, 128, 256):
+            assert 0 < bench.c_read_bytes_per_elem(k) < bench.bytes_per_elem(k, D), (k, D)
+    assert bench.c_read_bytes_per_elem("cost_h") == 0 and bench.c_read_bytes_per_elem("vfwd") == 0
+
+
+def test_source_sha_stable_and_complete():
+    a, b = bench.source_sha(), bench.source_sha()
+    assert a == b and len(a) == 16
+    # the PMC records name the source hash they were taken on
+    pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    for cfg in ("k128", "k128lr", "hd256", "4k256"):
+        tag = pmc["_tags"][cfg]
+        assert isinstance(tag, dict) and tag["src_sha"] and tag["git"], cfg
+
+
+def test_configs_cover_baseline():
+    # BASELINE.json configs: K64 (config 1), K128 V=1 (2), HD256 V=2 (3), 4K256 full (5)
+    c = bench.CONFIGS
+    assert (c["k64"]["D"], c["k64"]["views"]) == (64, 2)
+    assert (c["k128"]["D"], c["k128"]["views"]) == (128, 1)
+    assert (c["hd256"]["h"], c["hd256"]["w"], c["hd256"]["views"]) == (1080, 1920, 2)
+    assert c["4k256full"].get("full") and c["4k256full"]["D"] == 256
