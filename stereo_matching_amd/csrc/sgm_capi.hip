@@ -62,6 +62,7 @@ struct sgm_handle {
     bool t56;             // SGM_T56=1 (banded frames): T56 = L5 + L6 in the forward bands,
                           // L7 as a plain sweep in the backward bands (DESIGN.md lever 2)
     int fwd_band_rows;    // rows per forward band (a multiple of 16)
+    int mf_rows;          // median fill tile rows (4 or 8 by frame size; SGM_MF_ROWS)
     // post_filter scratch (sgm_post.hip)
     float *d_pf_orig;     // the map as it entered the median fill
     float *d_pf_work;     // contiguous working map (pitched callers)
@@ -749,7 +750,7 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st, bool to_
         for (int b = 0; b < batch; ++b, ++k)
             HIPCHK(h, timed(h, "post_median", dnpx, st, [&] {
                        return sgm::launch_median_fill(h->d_pf_orig, F, k, h->d_pf_snap,
-                                                      h->d_pf_changes, g, st);
+                                                      h->d_pf_changes, h->mf_rows, g, st);
                    }));
         HIPCHK(h, hipMemcpyAsync(h->h_pf_changes, h->d_pf_changes + k - 1, sizeof(int),
                                  hipMemcpyDeviceToHost, st));
@@ -839,6 +840,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
     const size_t npx = (size_t)h->g.H * h->g.W;
     const size_t nvol = npx * h->g.D;
     const size_t nin = (size_t)p->height * p->width;
+    h->mf_rows = sgm::median_rows_default(h->g);
     int rc = SGM_OK;
     do {
         if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
@@ -893,7 +895,6 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             h->sub_cm = !(cmv && *cmv == '0');
             const char *t = getenv("SGM_T56");
             h->t56 = h->fwd_bands && t && *t == '1';
-
         }
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {

@@ -143,8 +143,9 @@ hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st);
 hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream_t st);
 // post_filter (sgm_post.hip)
 size_t post_snapshot_floats(Geom g);
+int median_rows_default(Geom g);
 hipError_t launch_median_fill(const float *orig, float *F, int iter, float *snap, int *changes,
-                              Geom g, hipStream_t st);
+                              int rows, Geom g, hipStream_t st);
 hipError_t launch_pf_prep(const float *map, int pitch, float *orig, float *F, int *changes,
                           int nchanges, Geom g, hipStream_t st);
 hipError_t launch_cc_local(const float *F, int *L, int *cnt, int *area, Geom g, hipStream_t st);

@@ -7,7 +7,7 @@
 //    (i, j-2), (i, j-1)) and ORIGINAL values in the 12 cells after it.  Only
 //    pixels that were invalid on entry can change.  The result is the unique
 //    solution of that dependency DAG; it is computed here by
-//      * 64x16 tiles, one wave per tile, rows in order inside the tile with the
+//      * 64x4 or 64x8 tiles (by frame size), one wave per tile, rows in order inside the tile with the
 //        tile's window grid in LDS, and the in-row chain (j-1, j-2) resolved by
 //        iterating the row to its fixed point with lane shuffles;
 //      * chaotic relaxation across tiles: a tile reads its neighbours' border
@@ -23,16 +23,18 @@
 //    across tile borders in global memory (ECL-CC style: CAS on roots, pointer
 //    jumping on non-roots, larger root linked under smaller), per-tile counts
 //    folded into the roots' areas, then the area test.
+#include <cstdlib>
+
 #include "sgm_device.h"
 
 namespace sgm {
 namespace {
 
 constexpr int kMW = 64;        // median tile width: one lane per column
-constexpr int kMH = 16;        // median tile rows
 constexpr int kLW = kMW + 4;   // LDS row: two halo columns each side
 constexpr int kNoSample = 0x7fff;  // encodes an invalid sample (above any disparity)
-constexpr int kSnapN = 2 * kMW + 8 + 4 * kMH;  // working-map cells a tile reads (200)
+// working-map cells a tile of MH rows reads (200 at MH = 16)
+constexpr int snap_n(int MH) { return 2 * kMW + 8 + 4 * MH; }
 
 // Batcher's odd-even merge sort for 32 inputs, pruned to 22 (a comparator
 // touching a +inf pad is a no-op): 119 compare-exchanges, checked on all
@@ -192,19 +194,24 @@ __device__ __forceinline__ float shfl_up(float x, int d) {
 
 __device__ __forceinline__ int halo_col(int k) { return k < 2 ? k : kMW + k; }  // 0,1,66,67
 
+// MH tile rows (4, 8 or 16; median_rows_default): the tile's rows run in
+// order, so a launch's latency is MH row steps per round of resident tiles.
+template <int MH>
 __global__ __launch_bounds__(64) void median_fill_kernel(const float *__restrict__ orig,
                                                         float *__restrict__ F, int H, int W,
                                                         float dmax, int iter, float *snap,
                                                         int *changes) {
-    __shared__ float O[kMH + 4][kLW];   // window grid (rows r0-2 .. r0+kMH+1)
-    __shared__ float FL[kMH][2], FR[kMH][2];  // working-map halo columns of the tile rows
-    __shared__ float FC[kMH][kMW];            // the working map's tile cells (change test)
-    __shared__ int SF[22][kMW];               // each lane's sorted fixed samples of the row
+    static_assert(MH >= 2 && 4 * MH <= 64, "halo cells: one lane each");
+    constexpr int NOH = 4 * (MH + 2);      // original-map halo cells (4 columns x MH+2 rows)
+    __shared__ float O[MH + 4][kLW];       // window grid (rows r0-2 .. r0+MH+1)
+    __shared__ float FL[MH][2], FR[MH][2];  // working-map halo columns of the tile rows
+    __shared__ float FC[MH][kMW];           // the working map's tile cells (change test)
+    __shared__ int SF[22][kMW];             // each lane's sorted fixed samples of the row
     if (iter > 0 && changes[iter - 1] == 0) return;  // the last launch proved the fixed point
     const int tx = bid_x(), ty = bid_y(), ntx = (int)gridDim.x;
     const int tile = ty * ntx + tx;
     const int lane = tid_x();
-    const int r0 = ty * kMH, c0 = tx * kMW;
+    const int r0 = ty * MH, c0 = tx * kMW;
     const float out = dmax + 2.f;  // outside the frame: never a sample of an interior window
     auto at = [=](const float *m, int i, int j) {  // branch-free clamped load
         const float v = m[(size_t)clampi(i, 0, H - 1) * W + clampi(j, 0, W - 1)];
@@ -215,46 +222,50 @@ __global__ __launch_bounds__(64) void median_fill_kernel(const float *__restrict
     //    c0+64, c0+65 of the tile rows.  Unchanged since this tile's last
     //    launch (the snapshot) => its output is still its function of them.
     const int hk = lane & 3;
+    const bool hs_lane = lane < 4 * MH;  // lanes holding a tile-row halo cell
     const float h0 = at(F, r0 - 2, c0 + lane), h1 = at(F, r0 - 1, c0 + lane);
     const float hx = at(F, r0 - 2 + ((lane >> 2) & 1), c0 - 2 + halo_col(hk));  // lanes 0..7
     const float hs = at(F, r0 + (lane >> 2), c0 - 2 + halo_col(hk));
-    float *sn = snap + (size_t)tile * kSnapN;
+    float *sn = snap + (size_t)tile * snap_n(MH);
     if (iter > 0) {
         bool same = __float_as_uint(sn[lane]) == __float_as_uint(h0) &&
-                    __float_as_uint(sn[64 + lane]) == __float_as_uint(h1) &&
-                    __float_as_uint(sn[136 + lane]) == __float_as_uint(hs);
+                    __float_as_uint(sn[64 + lane]) == __float_as_uint(h1);
+        if (hs_lane) same = same && __float_as_uint(sn[136 + lane]) == __float_as_uint(hs);
         if (lane < 8) same = same && __float_as_uint(sn[128 + lane]) == __float_as_uint(hx);
         if (!__ballot(!same)) return;
     }
     sn[lane] = h0;
     sn[64 + lane] = h1;
-    sn[136 + lane] = hs;
+    if (hs_lane) sn[136 + lane] = hs;
     if (lane < 8) sn[128 + lane] = hx;
     // 2. The tile rows and the two rows below start as the original map
     //    (raster-later cells), plus the working map's own cells.
-    float ov[kMH + 2], fc[kMH], oh[2];
+    float ov[MH + 2], fc[MH], oh[2];
 #pragma unroll
-    for (int r = 0; r < kMH + 2; ++r) ov[r] = at(orig, r0 + r, c0 + lane);
+    for (int r = 0; r < MH + 2; ++r) ov[r] = at(orig, r0 + r, c0 + lane);
 #pragma unroll
-    for (int r = 0; r < kMH; ++r) fc[r] = at(F, r0 + r, c0 + lane);
+    for (int r = 0; r < MH; ++r) fc[r] = at(F, r0 + r, c0 + lane);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)  // 4 halo columns x 18 rows = 72 cells
+    for (int q = 0; q < 2; ++q)  // 4 halo columns x MH+2 rows
         oh[q] = at(orig, r0 + (lane + 64 * q) / 4, c0 - 2 + halo_col(hk));
     O[0][lane + 2] = h0;
     O[1][lane + 2] = h1;
     if (lane < 8) O[lane >> 2][halo_col(hk)] = hx;
-    if (hk < 2) FL[lane >> 2][hk] = hs; else FR[lane >> 2][hk - 2] = hs;
+    if (hs_lane) {
+        if (hk < 2) FL[lane >> 2][hk] = hs; else FR[lane >> 2][hk - 2] = hs;
+    }
 #pragma unroll
-    for (int r = 0; r < kMH + 2; ++r) O[r + 2][lane + 2] = ov[r];
+    for (int r = 0; r < MH + 2; ++r) O[r + 2][lane + 2] = ov[r];
 #pragma unroll
-    for (int r = 0; r < kMH; ++r) FC[r][lane] = fc[r];
-    O[2 + lane / 4][halo_col(hk)] = oh[0];
-    if (lane < 8) O[2 + (lane + 64) / 4][halo_col(hk)] = oh[1];
+    for (int r = 0; r < MH; ++r) FC[r][lane] = fc[r];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (lane + 64 * q < NOH) O[2 + (lane + 64 * q) / 4][halo_col(hk)] = oh[q];
     __syncthreads();
 
     const int j = c0 + lane, lc = lane + 2;
     bool changed_any = false;
-    for (int r = 0; r < kMH; ++r) {
+    for (int r = 0; r < MH; ++r) {
         const int i = r0 + r, lr = r + 2;
         if (i >= H) break;
         if (lane < 2) O[lr][lane] = FL[r][lane];   // (i, c0-2..c0-1) precede (i, c0)
@@ -513,15 +524,41 @@ __global__ __launch_bounds__(256) void pf_prep_kernel(const float *__restrict__ 
 
 }  // namespace
 
-size_t post_snapshot_floats(Geom g) {
-    return (size_t)((g.W + kMW - 1) / kMW) * ((g.H + kMH - 1) / kMH) * kSnapN;
+// Tile rows of the fill (read when a handle is created).  A launch takes
+// about MH row steps per round of tiles the chip holds at once (one wave each,
+// ~4k resident), so short tiles pay while their count stays within a round:
+// 4 rows when ceil(W/64) x ceil(H/4) <= 4096 tiles (K128: 43 vs 58 us at 8
+// rows per frame), else 8 (4K: 121 us; 150 at 4 rows, 149 at 16;
+// profiles/r03_experiments/median_tiles.txt).  SGM_MF_ROWS=4/8/16 forces it.
+int median_rows_default(Geom g) {
+    const char *e = std::getenv("SGM_MF_ROWS");
+    const int r = e ? std::atoi(e) : 0;
+    if (r == 4 || r == 8 || r == 16) return r;
+    return (size_t)((g.W + kMW - 1) / kMW) * ((g.H + 3) / 4) <= 4096 ? 4 : 8;
+}
+
+size_t post_snapshot_floats(Geom g) {  // enough for any tile height
+    const size_t tx = (size_t)(g.W + kMW - 1) / kMW;
+    size_t n = 0;
+    for (int mh : {4, 8, 16}) {
+        const size_t m = tx * ((g.H + mh - 1) / mh) * snap_n(mh);
+        n = m > n ? m : n;
+    }
+    return n;
+}
+
+template <int MH>
+static void launch_mf(const float *orig, float *F, int iter, float *snap, int *changes, Geom g,
+                      hipStream_t st) {
+    median_fill_kernel<MH><<<dim3((g.W + kMW - 1) / kMW, (g.H + MH - 1) / MH), 64, 0, st>>>(
+        orig, F, g.H, g.W, (float)(g.D - 1), iter, snap, changes);
 }
 
 hipError_t launch_median_fill(const float *orig, float *F, int iter, float *snap, int *changes,
-                              Geom g, hipStream_t st) {
-    const dim3 grid((g.W + kMW - 1) / kMW, (g.H + kMH - 1) / kMH);
-    hipLaunchKernelGGL(median_fill_kernel, grid, dim3(64), 0, st, orig, F, g.H, g.W,
-                       (float)(g.D - 1), iter, snap, changes);
+                              int rows, Geom g, hipStream_t st) {
+    if (rows == 16) launch_mf<16>(orig, F, iter, snap, changes, g, st);
+    else if (rows == 4) launch_mf<4>(orig, F, iter, snap, changes, g, st);
+    else launch_mf<8>(orig, F, iter, snap, changes, g, st);
     return hipGetLastError();
 }
 

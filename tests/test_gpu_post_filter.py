@@ -3,7 +3,7 @@
 The oracle (oracle/sgm_oracle.c:orc_post_filter) runs the reference's
 sequential in-place median fill and the single-thread semantics of
 speckle_filter_new; the GPU path (sgm_post.hip) must reproduce both exactly
-on every map, including fills that chain across its 64x16 tiles and
+on every map, including fills that chain across its 64x4 / 64x8 / 64x16 tiles and
 components that straddle the 1000/scale size limit.
 """
 from __future__ import annotations
@@ -42,6 +42,19 @@ def test_post_filter_maps(kind, hw):
     with SGM(H, W, 1, D, device=0) as sgm:
         for seed in range(2):
             check_map(sgm, postfilter_maps.make(kind, H, W, D, seed), D, 1)
+
+
+@pytest.mark.parametrize("rows", ["4", "8", "16"])
+@pytest.mark.parametrize("hw", [(61, 203), (375, 1242)], ids=["61x203", "375x1242"])
+def test_post_filter_tile_heights(rows, hw, monkeypatch):
+    """Every tile height of the median fill (the default picks 4 or 8 rows by
+    frame size; SGM_MF_ROWS forces one) gives the same bits."""
+    monkeypatch.setenv("SGM_MF_ROWS", rows)
+    H, W = hw
+    D = 64
+    with SGM(H, W, 1, D, device=0) as sgm:
+        for kind in postfilter_maps.KINDS:
+            check_map(sgm, postfilter_maps.make(kind, H, W, D, 3), D, 1)
 
 
 @pytest.mark.parametrize("D", [32, 128, 256])
