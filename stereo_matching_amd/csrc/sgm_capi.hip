@@ -733,7 +733,8 @@ int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st, bool to_
         HIPCHK(h, timed(h, "post_cc_merge", dnpx, st,
                         [&] { return sgm::launch_cc_merge(F, h->d_pf_label, g, st); }));
         HIPCHK(h, timed(h, "post_cc_count", dnpx, st, [&] {
-                   return sgm::launch_cc_count(h->d_pf_label, h->d_pf_count, h->d_pf_area, g, st);
+                   return sgm::launch_cc_count(h->d_pf_label, h->d_pf_count, h->d_pf_area, 1000 / g.scale,
+                                               g, st);
                }));
         // speckle_filter_new(filtered_disp, invalid_disp, SPECKLE_SIZE/scale, SPECKLE_DIS), :645
         HIPCHK(h, timed(h, "post_cc_apply", dnpx, st, [&] {

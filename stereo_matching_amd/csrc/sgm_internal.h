@@ -150,7 +150,8 @@ hipError_t launch_pf_prep(const float *map, int pitch, float *orig, float *F, in
                           int nchanges, Geom g, hipStream_t st);
 hipError_t launch_cc_local(const float *F, int *L, int *cnt, int *area, Geom g, hipStream_t st);
 hipError_t launch_cc_merge(const float *F, int *L, Geom g, hipStream_t st);
-hipError_t launch_cc_count(int *L, const int *cnt, int *area, Geom g, hipStream_t st);
+hipError_t launch_cc_count(int *L, const int *cnt, int *area, int max_size, Geom g,
+                           hipStream_t st);
 hipError_t launch_cc_apply(const float *F, const int *L, const int *area, int max_size,
                            float value, float *out, int out_pitch, Geom g, hipStream_t st);
 // LKRefine (sgm_lk.hip): left/right full-size images (decimated by g.scale on

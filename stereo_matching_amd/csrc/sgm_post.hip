@@ -7,9 +7,10 @@
 //    (i, j-2), (i, j-1)) and ORIGINAL values in the 12 cells after it.  Only
 //    pixels that were invalid on entry can change.  The result is the unique
 //    solution of that dependency DAG; it is computed here by
-//      * 64x4 or 64x8 tiles (by frame size), one wave per tile, rows in order inside the tile with the
-//        tile's window grid in LDS, and the in-row chain (j-1, j-2) resolved by
-//        iterating the row to its fixed point with lane shuffles;
+//      * 64x4 or 64x8 tiles (by frame size), one wave per tile, rows in order
+//        inside the tile with the tile's window grid in LDS, and the in-row
+//        chain (j-1, j-2) resolved by iterating the row to its fixed point
+//        with lane shuffles;
 //      * chaotic relaxation across tiles: a tile reads its neighbours' border
 //        cells from the working map as they are and keeps a snapshot of what
 //        it read; in the next launch it recomputes only if one of those cells
@@ -484,15 +485,20 @@ __global__ __launch_bounds__(128) void cc_merge_kernel(const float *__restrict__
 }
 
 // Tile-local roots: flatten to the final root and add their pixel counts.
+// Only area <= max_size matters to the test (cc_apply_kernel), and an area
+// only grows, so a root already read above max_size (even through a stale
+// line: a stale value is an older, smaller one) takes no more adds: the tile
+// roots of a frame-wide component (a road) no longer all add into one word.
 __global__ __launch_bounds__(256) void cc_count_kernel(int *L, const int *__restrict__ cnt,
-                                                      int *area, int n) {
+                                                      int *area, int n, int max_size) {
     const int k = bid_x() * 256 + tid_x();
     if (k >= n) return;
     const int c = cnt[k];
     if (c == 0) return;
     const int root = g_find(L, k);
     atomicMin(L + k, root);
-    atomicAdd(area + root, c);
+    if (__hip_atomic_load(area + root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= max_size)
+        atomicAdd(area + root, c);
 }
 
 // speckle_filter_new's last loop (:556-565): components of at most max_size
@@ -582,9 +588,11 @@ hipError_t launch_cc_merge(const float *F, int *L, Geom g, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_cc_count(int *L, const int *cnt, int *area, Geom g, hipStream_t st) {
+hipError_t launch_cc_count(int *L, const int *cnt, int *area, int max_size, Geom g,
+                           hipStream_t st) {
     const int n = g.H * g.W;
-    hipLaunchKernelGGL(cc_count_kernel, dim3((n + 255) / 256), dim3(256), 0, st, L, cnt, area, n);
+    hipLaunchKernelGGL(cc_count_kernel, dim3((n + 255) / 256), dim3(256), 0, st, L, cnt, area, n,
+                       max_size);
     return hipGetLastError();
 }
 
