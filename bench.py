@@ -170,6 +170,10 @@ def parse():
                     help="end each step with LKRefine on the GPU (SGM.cpp:824, LKSubPixelImpl.cpp)")
     ap.add_argument("--sky-detect", action="store_true",
                     help="start each step with the sky detector on both views (node.cpp:80-93)")
+    ap.add_argument("--gather-every", type=int, default=1,
+                    help="N > 1: gather the maps of this many steps in one collective")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="diagnostic: N > 1 without the gather of the maps (not a valid bench line)")
     ap.add_argument("--view-split", action="store_true",
                     help="N even, V=2 configs: one pair per two GPUs, left view on the even rank, "
                          "right view on the odd one, F_R over RCCL point-to-point (SURVEY.md 8e "
@@ -213,9 +217,11 @@ def main():
     # N > 1: each step's map goes to rank 0 by a gather that overlaps the next
     # step's kernels (double-buffered maps, stereo_matching_amd.distributed)
     pipe = None
-    if distributed and not args.view_split:
+    gk = max(1, args.gather_every)
+    if distributed and not args.view_split and not args.no_gather:
         from stereo_matching_amd.distributed import PipelinedGather
-        pipe = PipelinedGather((h, w), torch.float32, dev, depth=2)
+        pipe = PipelinedGather((gk, h, w) if gk > 1 else (h, w), torch.float32, dev, depth=2)
+    nstep = [0]
 
     if cfg.get("full"):
         args.post_filter = args.lk_refine = args.sky_detect = True
@@ -238,14 +244,24 @@ def main():
         if team:
             team.step(d_left.data_ptr(), d_right.data_ptr(), d_out)
             return
-        out = pipe.buffer() if pipe else d_out
+        out = d_out
+        if pipe:
+            out = pipe.buffer()
+            out = out[nstep[0] % gk] if gk > 1 else out
         sgm.process_device(d_left.data_ptr(), d_right.data_ptr(), out.data_ptr(),
                            stream=stream.cuda_stream)
-        if pipe:
+        nstep[0] += 1
+        if pipe and nstep[0] % gk == 0:
             pipe.submit()
+
+    def flush():  # a partial batch of maps goes out before a drain
+        if pipe and nstep[0] % gk:
+            pipe.submit()
+        nstep[0] = 0
 
     for _ in range(args.warmup):
         step()
+    flush()
     if pipe:
         pipe.drain()
     torch.cuda.synchronize(dev)
@@ -257,6 +273,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(k):
             step()
+        flush()
         if pipe:
             pipe.drain()  # every gather of the timed steps is inside the timed region
         torch.cuda.synchronize(dev)
@@ -429,8 +446,12 @@ def main():
                        "parallelism": (f"view-split x{pairs} (left/right view per GPU, F_R over "
                                        f"RCCL point-to-point; maps stay on the even ranks)"
                                        if args.view_split else
-                                       f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0 "
-                                       f"overlapped with the next step" if distributed else
+                                       (f"pair-sharded x{world} (1 pair/GPU), NO gather (diagnostic)"
+                                        if args.no_gather else
+                                        f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0 "
+                                        + (f"of every {gk} steps' maps in one collective, "
+                                           if gk > 1 else "")
+                                        + "overlapped with the next step") if distributed else
                                        "1 pair on 1 GPU (single process: no process group, no "
                                        "gather)")},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
