@@ -634,9 +634,6 @@ __device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*
         const float lim = (Dn - 1) * 1.f;
         f = (lim < xx) ? lim : xx;  // std::min(x, lim)
     }
-#ifdef SGM_PROBE_NO_FINAL_STORES  // timing probe only (wrong results): bounds what the
-    cnt = d == -7 ? cnt : 0;       // outputs' partial-line writes cost the final pass
-#endif
     if (q == 0 && px < cnt) {
         // disp: only when the frame hands out its raw WTA map (else null:
         // these one-pixel-per-row stores are partial cache lines, ~5% of the
