@@ -234,10 +234,13 @@ def main():
     else:
         sgm = SGM(h, w, 1, D, views=views, device=local, post_filter=args.post_filter,
                   lk_refine=args.lk_refine, sky_detect=args.sky_detect)
-    # one explicit stream for everything a step enqueues (the library's
-    # kernels, torch's copies, RCCL's stream dependencies)
+    # one stream for everything a step enqueues (the library's kernels,
+    # torch's copies, RCCL's stream dependencies): the handle's own stream
+    # (sgm_get_stream), so the library's calls record no events (a call on a
+    # caller's stream records one as it returns: a ~5 us gap before the next
+    # frame's first kernel)
     torch.cuda.synchronize(dev)
-    stream = torch.cuda.Stream(dev)
+    stream = torch.cuda.ExternalStream(sgm.stream, device=dev)
     torch.cuda.set_stream(stream)
 
     def step():

@@ -27,9 +27,11 @@
  * volumes, checkpoints, post-filter and LKRefine buffers), so the library
  * orders calls made on different streams: a call whose stream differs from
  * the previous call's first makes its stream wait for the previous call's
- * work (an event it records on the previous call's stream, which must
- * therefore still exist).  Calls on one stream are ordered by the stream
- * itself and record nothing.  Device entry points return after
+ * work.  A call on a caller's stream records an event on that stream as it
+ * returns (so the library keeps no caller stream past the call that used
+ * it; the record costs the next kernel on that stream a ~5 us dispatch
+ * gap); calls on the handle's own stream (NULL, sgm_get_stream) record
+ * nothing.  Device entry points return after
  * enqueueing, EXCEPT with post_filter: its median fill blocks the calling
  * host thread on an event once per two fill launches to read a convergence
  * counter (sgm_post_filter_device, and sgm_process_device with
@@ -136,6 +138,13 @@ const char *sgm_last_error(const sgm_handle *h);
 int sgm_get_size(const sgm_handle *h, int *rows, int *cols, int *max_disp);
 /* Bytes of device memory the handle holds. */
 size_t sgm_device_bytes(const sgm_handle *h);
+/* The handle's own stream (a hipStream_t; what a NULL stream argument
+ * means), valid until sgm_destroy; NULL for a NULL handle.  A caller that
+ * runs its own work around the handle's calls can enqueue it on this stream
+ * (e.g. as torch.cuda.ExternalStream) and pass NULL: calls on the handle's
+ * stream record no events, while a call on a caller's stream records one as
+ * it returns (see "Streams" above). */
+void *sgm_get_stream(const sgm_handle *h);
 
 /*
  * SGM::process(l, r, sky, sky_beta) (src/SGM.cpp:32-826, :829-834) up to and

@@ -33,7 +33,7 @@ EXPORTS = (
     "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
     "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine", "sgm_sky_detect_device",
     "sgm_stage_sky_detect", "sgm_colormap_device", "sgm_point_cloud_device", "sgm_stage_colormap",
-    "sgm_stage_point_cloud", "sgm_lr_check_device",
+    "sgm_stage_point_cloud", "sgm_lr_check_device", "sgm_get_stream",
 )
 
 
@@ -98,6 +98,8 @@ def lib():
     L.sgm_get_size.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)]
     L.sgm_device_bytes.argtypes = [P]
     L.sgm_device_bytes.restype = ctypes.c_size_t
+    L.sgm_get_stream.argtypes = [P]
+    L.sgm_get_stream.restype = ctypes.c_void_p
     L.sgm_process.argtypes = [P, P, P, I, P, P, I, P, I, P]
     L.sgm_process_device.argtypes = [P, P, P, I, P, P, I, P, I, P, P]
     L.sgm_post_filter_device.argtypes = [P, P, I, P]
@@ -120,7 +122,7 @@ def lib():
     L.sgm_set_profiling.argtypes = [P, I]
     L.sgm_get_profile.argtypes = [P, ctypes.POINTER(KernelStat), I, ctypes.POINTER(I)]
     for name in EXPORTS:
-        if name not in ("sgm_last_error", "sgm_device_bytes"):
+        if name not in ("sgm_last_error", "sgm_device_bytes", "sgm_get_stream"):
             getattr(L, name).restype = I
     _lib = L
     return L

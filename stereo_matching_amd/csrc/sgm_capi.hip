@@ -104,16 +104,13 @@ struct DeviceGuard {
 
 // Every entry point's work shares the handle's scratch (cost volumes,
 // checkpoints, post-filter and LKRefine buffers), whichever stream the caller
-// passes.  A StreamScope orders calls on different streams: if this call's
-// stream differs from the previous call's, it records an event on the
-// previous stream -- behind everything enqueued there so far, the previous
-// call's work included -- and makes its own stream wait for it.  Calls on one
-// stream record nothing (an event record costs the next kernel a ~5 us
-// dispatch gap: the gap between back-to-back frames in the rocprof trace).
+// passes.
 // Orders calls on different streams (they share the handle's scratch).  A
 // call on a CALLER's stream records ev_last on that stream as it returns,
-// while the stream certainly exists; a call on the handle's own stream records
-// nothing (the same-stream path stays free of event records) and a later
+// while the stream certainly exists (the record costs the next kernel on that
+// stream a ~5 us dispatch gap: callers that run back-to-back frames use the
+// handle's own stream, sgm_get_stream); a call on the handle's own stream
+// records nothing (the same-stream path stays free of event records) and a later
 // call on another stream records ev_last on the handle's stream, which the
 // handle owns.  So no stream handle of the caller is kept past the call that
 // used it.  Entry points construct the scope after their argument checks, so
@@ -956,6 +953,8 @@ int sgm_get_size(const sgm_handle *h, int *rows, int *cols, int *max_disp) {
 }
 
 size_t sgm_device_bytes(const sgm_handle *h) { return h ? h->bytes : 0; }
+
+void *sgm_get_stream(const sgm_handle *h) { return h ? (void *)h->st : nullptr; }
 
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,

@@ -108,6 +108,13 @@ class SGM:
     def device_bytes(self) -> int:
         return int(self._lib.sgm_device_bytes(self._h))
 
+    @property
+    def stream(self) -> int:
+        """The handle's own stream (sgm_get_stream), as an integer hipStream_t
+        for torch.cuda.ExternalStream: work on it is ordered with the calls
+        made with stream=None, and those calls record no events."""
+        return int(self._lib.sgm_get_stream(self._h) or 0)
+
     # ------------------------------------------------------------ process
     def process(self, img_l, img_r, sky_mask=None, sky_mask_beta=None) -> None:
         """SGM::process (src/SGM.cpp:32-826, sky overload :829-834)."""

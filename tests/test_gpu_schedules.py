@@ -108,6 +108,23 @@ with SGM(h, w, 1, D, device=0) as sgm:
 for k, out in enumerate(outs):
     got = out.cpu().numpy()
     assert np.array_equal(got.view(np.uint32), want[k].view(np.uint32)), k
+# the handle's own stream (sgm_get_stream) as torch's stream, mixed with NULL
+# and a caller's stream: torch work on it is ordered with the handle's calls
+outs2 = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in pairs]
+with SGM(h, w, 1, D, device=0) as sgm:
+    assert sgm.stream != 0
+    hs = torch.cuda.ExternalStream(sgm.stream, device=dev)
+    for k, ((l, r), out) in enumerate(zip(imgs, outs2)):
+        with torch.cuda.stream(hs):
+            out.fill_(-1.0)
+        st = (hs.cuda_stream, None, streams[k % 3].cuda_stream, None)[k]
+        if st not in (None, hs.cuda_stream):
+            out.record_stream(streams[k % 3])
+        sgm.process_device(l.data_ptr(), r.data_ptr(), out.data_ptr(), stream=st)
+        sgm.post_filter_device(out.data_ptr(), stream=None)
+    torch.cuda.synchronize(dev)
+for k, out in enumerate(outs2):
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want[k].view(np.uint32)), k
 print("cross-stream ok")
 """
 
