@@ -20,7 +20,7 @@ print('$c', r['value'], 'MPD/s', r['ms_per_step'], 'ms', 'roof', r['roofline']['
       bash tools/prof_full.sh $TAG $c | tail -2 || exit 1
     done ;;
   pmc)
-    for c in k128 k64 k128lr hd256 4k256 k128full; do
+    for c in k128 k64 k128lr hd256 4k256 k128full 4k256full; do
       bash tools/pmc.sh $TAG $c > gpurun_out/${TAG}_pmc_$c.txt 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_$c.txt; exit 1; }
       echo "pmc $c done"
     done ;;
