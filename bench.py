@@ -174,6 +174,9 @@ def parse():
                     help="N > 1: gather the maps of this many steps in one collective")
     ap.add_argument("--no-gather", action="store_true",
                     help="diagnostic: N > 1 without the gather of the maps (not a valid bench line)")
+    ap.add_argument("--caller-stream", action="store_true",
+                    help="diagnostic: run the frames on a stream of the caller's instead of the "
+                         "handle's own (each call then records an event as it returns)")
     ap.add_argument("--view-split", action="store_true",
                     help="N even, V=2 configs: one pair per two GPUs, left view on the even rank, "
                          "right view on the odd one, F_R over RCCL point-to-point (SURVEY.md 8e "
@@ -240,7 +243,8 @@ def main():
     # caller's stream records one as it returns: a ~5 us gap before the next
     # frame's first kernel)
     torch.cuda.synchronize(dev)
-    stream = torch.cuda.ExternalStream(sgm.stream, device=dev)
+    stream = (torch.cuda.Stream(dev) if args.caller_stream
+              else torch.cuda.ExternalStream(sgm.stream, device=dev))
     torch.cuda.set_stream(stream)
 
     def step():

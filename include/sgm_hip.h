@@ -29,8 +29,8 @@
  * the previous call's first makes its stream wait for the previous call's
  * work.  A call on a caller's stream records an event on that stream as it
  * returns (so the library keeps no caller stream past the call that used
- * it; the record costs the next kernel on that stream a ~5 us dispatch
- * gap); calls on the handle's own stream (NULL, sgm_get_stream) record
+ * it; a rocprof trace shows the record as a ~5 us gap before the next
+ * kernel); calls on the handle's own stream (NULL, sgm_get_stream) record
  * nothing.  Device entry points return after
  * enqueueing, EXCEPT with post_filter: its median fill blocks the calling
  * host thread on an event once per two fill launches to read a convergence

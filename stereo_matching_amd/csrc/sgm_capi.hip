@@ -107,9 +107,9 @@ struct DeviceGuard {
 // passes.
 // Orders calls on different streams (they share the handle's scratch).  A
 // call on a CALLER's stream records ev_last on that stream as it returns,
-// while the stream certainly exists (the record costs the next kernel on that
-// stream a ~5 us dispatch gap: callers that run back-to-back frames use the
-// handle's own stream, sgm_get_stream); a call on the handle's own stream
+// while the stream certainly exists (a rocprof trace shows the record as a
+// ~5 us gap before the next kernel; frame loops can run on the handle's own
+// stream, sgm_get_stream, instead); a call on the handle's own stream
 // records nothing (the same-stream path stays free of event records) and a later
 // call on another stream records ev_last on the handle's stream, which the
 // handle owns.  So no stream handle of the caller is kept past the call that
