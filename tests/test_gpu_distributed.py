@@ -156,16 +156,22 @@ def test_two_gloo_ranks_on_one_gpu():
 
 
 @pytest.mark.timeout(300)
-def test_bench_under_torch_distributed_run():
+@pytest.mark.parametrize("extra", [[], ["--gather-every", "3"], ["--caller-stream"]],
+                         ids=["gather_every_step", "gather_every_3", "caller_stream"])
+def test_bench_under_torch_distributed_run(extra):
     # the driver's multi-GPU launch line at N = 1: process group on nccl
     # (RCCL), the pipelined gather of every step's map inside the timed region
+    # (and the batched gather, with a partial last batch: 5 timed steps in
+    # batches of 3; and the frames on a caller's stream)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", _port(), os.path.join(ROOT, "bench.py"),
-           "--gpus", "1", "--steps", "4", "--warmup", "2", "--no-profile-pass"]
+           "--gpus", "1", "--steps", "5", "--warmup", "2", "--no-profile-pass"] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     rec = json.loads(line)
     assert rec["n_gpus"] == 1 and rec["value"] > 0
     assert "RCCL" in rec["config"]["parallelism"]
+    if extra[:1] == ["--gather-every"]:
+        assert "every 3 steps" in rec["config"]["parallelism"]
     assert rec["cpu_baseline"] is not None
