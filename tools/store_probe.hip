@@ -7,6 +7,11 @@
 //      (a 256 B store per wave-step, the pixel's other half from the other wave)
 //   B: one wave per row, two disparities per lane: one 512 B dwordx2 store per step
 //   C: like A, but both waves of a row in one workgroup of one row only
+//   D: like A, but every 4 steps one dwordx4 store per lane (16 lanes per
+//      pixel's 64 disparities, 4 pixels per 1 KB wave-instruction), the
+//      4x64 block transposed through LDS
+//   E: A with default-policy (cached) stores
+//   F: the flat float4 stream (grid-stride), the volume's write ceiling
 // Usage: hipcc -O3 --offload-arch=gfx950 tools/store_probe.hip -o /tmp/store_probe && /tmp/store_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -50,6 +55,56 @@ __global__ __launch_bounds__(64) void pat_b(float *__restrict__ o) {
     }
 }
 
+// D: lane = d for the chain; every 4 steps a 64 x 4 block goes through LDS
+template <int DELAY>
+__global__ __launch_bounds__(256) void pat_d(float *__restrict__ o) {
+    __shared__ float tile[4][4][68];  // per wave: 4 steps x 64 d (+pad)
+    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int r = threadIdx.x / D, d = threadIdx.x % D;
+    const int i = blockIdx.x * 2 + r;
+    if (i >= H) return;
+    float x = (float)d;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int dbase = d - lane;  // 0 or 64
+    float *prow = o + (long long)i * W * D + dbase + 4 * (lane % 16);
+    for (int j = 0; j + 4 <= W; j += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            x = work<DELAY>(x);
+            tile[wv][u][lane] = x;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int u = lane / 16, q = 4 * (lane % 16);
+        f4 v = {tile[wv][u][q], tile[wv][u][q + 1], tile[wv][u][q + 2], tile[wv][u][q + 3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(prow + (long long)(j + u) * D));
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <int DELAY>
+__global__ __launch_bounds__(256) void pat_e(float *__restrict__ o, int R) {
+    const int r = threadIdx.x / D, d = threadIdx.x % D;
+    const int i = blockIdx.x * R + r;
+    if (i >= H) return;
+    float x = (float)d;
+    float *p = o + (long long)i * W * D + d;
+    for (int j = 0; j < W; ++j) {
+        x = work<DELAY>(x);
+        p[(long long)j * D] = x;
+    }
+}
+
+__global__ __launch_bounds__(256) void pat_f(float *__restrict__ o) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4 *p = reinterpret_cast<f4 *>(o);
+    const long long n4 = N / 4;
+    for (long long k = blockIdx.x * 256ll + threadIdx.x; k < n4; k += (long long)gridDim.x * 256) {
+        f4 v = {(float)k, 1.f, 2.f, 3.f};
+        __builtin_nontemporal_store(v, p + k);
+    }
+}
+
 template <typename F>
 static float time_it(F f) {
     hipEvent_t a, b;
@@ -72,6 +127,10 @@ static void run(float *o) {
     const float ta2 = time_it([&] { pat_a<DELAY><<<(H + 1) / 2, 2 * D>>>(o, 2); });
     const float ta1 = time_it([&] { pat_a<DELAY><<<H, D>>>(o, 1); });
     const float tb = time_it([&] { pat_b<DELAY><<<H, 64>>>(o); });
+    const float td = time_it([&] { pat_d<DELAY><<<(H + 1) / 2, 2 * D>>>(o); });
+    const float te = time_it([&] { pat_e<DELAY><<<(H + 1) / 2, 2 * D>>>(o, 2); });
+    printf("delay %3d  D (dwordx4 via LDS) %7.1f us %5.2f TB/s | E (A, cached) %7.1f us %5.2f TB/s\n",
+           DELAY, td, bytes / td / 1e6, te, bytes / te / 1e6);
     printf("delay %3d  A (2 rows/WG, 4 waves, 256 B/store) %7.1f us %5.2f TB/s | "
            "C (1 row/WG) %7.1f us %5.2f TB/s | B (1 wave/row, 512 B dwordx2) %7.1f us %5.2f TB/s\n",
            DELAY, ta2, bytes / ta2 / 1e6, ta1, bytes / ta1 / 1e6, tb, bytes / tb / 1e6);
@@ -80,6 +139,8 @@ static void run(float *o) {
 int main() {
     float *o;
     if (hipMalloc(&o, N * sizeof(float)) != hipSuccess) return 1;
+    const float tf = time_it([&] { pat_f<<<4096, 256>>>(o); });
+    printf("F (flat float4 nt stream) %7.1f us %5.2f TB/s\n", tf, (double)N * 4 / tf / 1e6);
     run<0>(o);
     run<4>(o);
     run<8>(o);
