@@ -1,5 +1,5 @@
 """Pair sharding + gather to rank 0 (stereo_matching_amd/distributed.py) with
-world_size 2 on the gloo backend (CPU).  Each rank computes its pairs with the
+world_size 2 (and 8, config 4's batch) on the gloo backend (CPU).  Each rank computes its pairs with the
 oracle (test infrastructure) on tiny synthetic pairs; rank 0 checks the
 gathered batch against a single-process run."""
 from __future__ import annotations
@@ -85,6 +85,28 @@ def test_gather_world2_gloo(n):
         assert np.array_equal(res[0].view(np.uint32), want.view(np.uint32))
 
 
+def test_config4_batch_of_8_world8_gloo():
+    # BASELINE config 4's shape: a batch of 8 pairs, one per rank on 8 ranks,
+    # maps gathered to rank 0 in pair order (the RCCL path carries the same
+    # calls; 8-GPU runs are the driver's)
+    import oracle
+    oracle.build()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 8, port, q, 8)) for r in range(8)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r] is None for r in range(1, 8))
+    want = np.stack([_compute(p).numpy() for p in _pairs(8)])
+    assert res[0].shape == (8, H, W)
+    assert np.array_equal(res[0].view(np.uint32), want.view(np.uint32))
+
+
 def _pipe_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -106,13 +128,14 @@ def _pipe_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_pipelined_gather_world2_gloo():
+@pytest.mark.parametrize("world", [2, 8])
+def test_pipelined_gather_gloo(world):
     # bench.py's overlapped per-step gather: every step's maps reach rank 0
     # intact although the next step already writes the other buffer
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -121,7 +144,8 @@ def test_pipelined_gather_world2_gloo():
         assert p.exitcode == 0
     assert sorted(res[0]) == [0, 1, 2, 3, 4]
     for k, maps in res[0].items():
-        for r in range(2):
+        assert len(maps) == world
+        for r in range(world):
             assert (maps[r] == 100 * r + k).all(), (k, r)
 
 
