@@ -453,8 +453,11 @@ hipError_t launch_sky_detect(const uint8_t *const *img, int pitch, uint8_t *cons
     const int half = g.H / 2, last = half < g.H - 1 ? half : g.H - 1;
     const size_t strip = SkyLds(last).bytes;
     if (strip > kSkyStripMax) return hipErrorInvalidValue;  // H > ~4700 rows
+    // the kernel's dynamic-LDS ceiling is one value for the whole process:
+    // always the same maximum, so handles of other frame sizes running on
+    // other host threads can never lower it under this launch
     hipError_t e = hipFuncSetAttribute((const void *)sky_columns_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)strip);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSkyStripMax);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sky_columns_kernel, dim3((g.W + kSkyCols - 1) / kSkyCols, 1, nviews),
                        dim3(256), strip, st,
