@@ -170,7 +170,10 @@ def parse():
                     help="end each step with LKRefine on the GPU (SGM.cpp:824, LKSubPixelImpl.cpp)")
     ap.add_argument("--sky-detect", action="store_true",
                     help="start each step with the sky detector on both views (node.cpp:80-93)")
-    ap.add_argument("--gather-every", type=int, default=1,
+    # 4: one collective per 4 steps' maps measured 1.9% faster per step than one per step
+    # under torchrun at world 1 (profiles/r03_experiments/gather_batching.txt); the
+    # last batch's gather runs after the last step (~50 us at N = 8 per timed region)
+    ap.add_argument("--gather-every", type=int, default=4,
                     help="N > 1: gather the maps of this many steps in one collective")
     ap.add_argument("--no-gather", action="store_true",
                     help="diagnostic: N > 1 without the gather of the maps (not a valid bench line)")

@@ -156,13 +156,15 @@ def test_two_gloo_ranks_on_one_gpu():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("extra", [[], ["--gather-every", "3"], ["--caller-stream"]],
-                         ids=["gather_every_step", "gather_every_3", "caller_stream"])
+@pytest.mark.parametrize("extra", [[], ["--gather-every", "1"], ["--gather-every", "3"],
+                                   ["--caller-stream"]],
+                         ids=["default", "gather_every_step", "gather_every_3", "caller_stream"])
 def test_bench_under_torch_distributed_run(extra):
     # the driver's multi-GPU launch line at N = 1: process group on nccl
-    # (RCCL), the pipelined gather of every step's map inside the timed region
-    # (and the batched gather, with a partial last batch: 5 timed steps in
-    # batches of 3; and the frames on a caller's stream)
+    # (RCCL), the pipelined gather of the maps inside the timed region (the
+    # default batches 4 steps' maps per collective: 5 timed steps end on a
+    # partial batch; also one gather per step, batches of 3, and the frames
+    # on a caller's stream)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", _port(), os.path.join(ROOT, "bench.py"),
            "--gpus", "1", "--steps", "5", "--warmup", "2", "--no-profile-pass"] + extra
@@ -172,6 +174,11 @@ def test_bench_under_torch_distributed_run(extra):
     rec = json.loads(line)
     assert rec["n_gpus"] == 1 and rec["value"] > 0
     assert "RCCL" in rec["config"]["parallelism"]
-    if extra[:1] == ["--gather-every"]:
-        assert "every 3 steps" in rec["config"]["parallelism"]
+    par = rec["config"]["parallelism"]
+    if extra == ["--gather-every", "3"]:
+        assert "every 3 steps" in par
+    elif extra == ["--gather-every", "1"]:
+        assert "every" not in par and "overlapped with the next step" in par
+    else:
+        assert "every 4 steps" in par
     assert rec["cpu_baseline"] is not None
