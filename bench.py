@@ -461,7 +461,8 @@ def main():
                                         f"pair-sharded x{world} (1 pair/GPU), RCCL gather to rank 0 "
                                         + (f"of every {gk} steps' maps in one collective, "
                                            if gk > 1 else "")
-                                        + "overlapped with the next step") if distributed else
+                                        + ("overlapped with the following steps" if gk > 1
+                                           else "overlapped with the next step")) if distributed else
                                        "1 pair on 1 GPU (single process: no process group, no "
                                        "gather)")},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
