@@ -180,6 +180,9 @@ def parse():
     ap.add_argument("--caller-stream", action="store_true",
                     help="diagnostic: run the frames on a stream of the caller's instead of the "
                          "handle's own (each call then records an event as it returns)")
+    ap.add_argument("--graph", action="store_true",
+                    help="single process: time replays of one frame captured as a HIP graph "
+                         "(the per-kernel profile pass still runs eagerly)")
     ap.add_argument("--view-split", action="store_true",
                     help="N even, V=2 configs: one pair per two GPUs, left view on the even rank, "
                          "right view on the odd one, F_R over RCCL point-to-point (SURVEY.md 8e "
@@ -275,6 +278,20 @@ def main():
     if pipe:
         pipe.drain()
     torch.cuda.synchronize(dev)
+    eager_step = step
+    if args.graph:
+        # the frame's launches recorded once on the handle's stream (no event
+        # records there, so the whole frame is capturable) and replayed as one
+        # graph launch per step
+        if pipe or team:
+            raise SystemExit("--graph: single-process runs only")
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+            eager_step()
+        torch.cuda.synchronize(dev)
+
+        def step():
+            graph.replay()
 
     def timed_steps(k):
         if distributed:
@@ -307,6 +324,7 @@ def main():
     kernels = {}
     if not args.no_profile_pass:
         sgm.set_profiling(True)
+        step = eager_step
         prof_elapsed = timed_steps(args.steps)
         prof = sgm.get_profile()
         sgm.set_profiling(False)
@@ -452,6 +470,7 @@ def main():
                        "width": w, "height": h, "max_disp": D, "views": views,
                        "post_filter": bool(args.post_filter), "lk_refine": bool(args.lk_refine),
                        "sky_detect": bool(args.sky_detect),
+                       "launch": "one HIP graph replay per frame" if args.graph else "eager",
                        "pairs_per_gpu": 0.5 if args.view_split else 1, "global_batch": pairs,
                        "parallelism": (f"view-split x{pairs} (left/right view per GPU, F_R over "
                                        f"RCCL point-to-point; maps stay on the even ranks)"
