@@ -1,0 +1,56 @@
+"""A frame captured once as a HIP graph (torch.cuda.graph on the handle's own
+stream) and replayed: the replay computes what an eager sgm_process_device
+call computes, from whatever the captured input buffers hold at replay time
+(a serving loop that refills fixed buffers).  bench.py --graph times this;
+profiles/r03_experiments/hip_graph.txt measured it equal to eager launches."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from stereo_matching_amd import SGM, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("h,w,D,views,sky", [(96, 320, 64, 2, False), (375, 1242, 128, 1, False),
+                                             (120, 256, 128, 2, True)])
+def test_frame_replays_from_a_hip_graph(h, w, D, views, sky):
+    dev = torch.device("cuda", 0)
+    with SGM(h, w, 1, D, views=views) as sgm:
+        stream = torch.cuda.ExternalStream(sgm.stream, device=dev)
+        d_l = torch.empty((h, w), dtype=torch.uint8, device=dev)
+        d_r = torch.empty_like(d_l)
+        d_sky = torch.from_numpy(synthetic.sky_mask(h, w)).to(dev) if sky else None
+        skyp = d_sky.data_ptr() if sky else 0
+        out_e = torch.empty((h, w), dtype=torch.float32, device=dev)
+        out_g = torch.empty_like(out_e)
+
+        def frame(out):
+            sgm.process_device(d_l.data_ptr(), d_r.data_ptr(), out.data_ptr(), d_sky_l=skyp,
+                               d_sky_r=skyp if views == 2 else 0, stream=stream.cuda_stream)
+
+        def load(k):
+            left, right = synthetic.stereo_pair(h, w, D, pair_index=k)
+            with torch.cuda.stream(stream):
+                d_l.copy_(torch.from_numpy(left))
+                d_r.copy_(torch.from_numpy(right))
+
+        load(0)
+        with torch.cuda.stream(stream):
+            frame(out_e)  # warm-up (the capture needs no first-call work)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+            frame(out_g)
+        torch.cuda.synchronize(dev)
+        for k in (1, 2, 3):
+            load(k)
+            with torch.cuda.stream(stream):
+                graph.replay()
+                frame(out_e)
+            torch.cuda.synchronize(dev)
+            g, e = out_g.cpu().numpy(), out_e.cpu().numpy()
+            assert np.array_equal(g.view(np.uint32), e.view(np.uint32)), k
