@@ -84,7 +84,9 @@ typedef struct sgm_params {
     int max_disp;      /* D in {32,64,128,256} (Solver.cpp:10, widened)          */
     int p1;            /* 10  (SGM.cpp:27) */
     int p2;            /* 100 (SGM.cpp:28) */
-    float uniqueness;  /* 0.7 UNIQUE_RATIO (inc/Solver.h:14) */
+    float uniqueness;  /* 0.7 UNIQUE_RATIO (inc/Solver.h:14); must exceed 8*(p2+999999)/FLT_MAX
+                          (about 2e-32): at or below it the reference's WTA would read the
+                          previous pixel's sec_min_d (SGM.cpp:392-408), so sgm_create rejects it */
     float lr_max_diff; /* 1.0 LR_CHECK_DIS (inc/Solver.h:16) */
     int blur;          /* 1: pre-blur as Solver.cpp:124-125 (pinned formula); 0: off */
     int views;         /* 2: left+right views + LR check (SGM.cpp:32-818); 1: left view only */

@@ -16,6 +16,7 @@
 #include "sgm_internal.h"
 
 #include <algorithm>
+#include <float.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -45,8 +46,7 @@ struct sgm_handle {
     uint64_t *d_ct[2];    // census words
     float *d_ch[2];       // horizontally filtered cost; reused as the T chain
     float *d_ch_base[2];  // its allocation: d_ch is preceded by t_guard_rows rows (final pass)
-    float *d_c[2];        // final cost volume
-    float *d_c_base[2];   // its allocation
+    float *d_c[2];        // final cost volume (+ kVolGuard: row-walking prefetch rings)
     float *d_s[2];        // S chain
     uint16_t *d_disp[2];  // WTA disparity
     float *d_sub[2];      // sub-pixel disparity
@@ -168,10 +168,19 @@ bool valid_params(const sgm_params *p, char *why, size_t n) {
     if (W < 5 || H < 3) { snprintf(why, n, "working size %dx%d below the 5x3 cost window", H, W); return false; }
     if (p->views != 1 && p->views != 2) { snprintf(why, n, "views must be 1 or 2"); return false; }
     // SGM.cpp:374-408 keeps the previous pixel's sec_min_d when a pixel has no
-    // second distinct cost; that stale index can decide a pixel only when
-    // min/FLT_MAX > UNIQUE_RATIO, i.e. for a negative ratio, which this build
-    // therefore rejects (its WTA keeps no state across pixels)
-    if (!(p->uniqueness >= 0.0f)) { snprintf(why, n, "uniqueness must be >= 0"); return false; }
+    // second distinct cost; that stale index decides a pixel when
+    // min/FLT_MAX > UNIQUE_RATIO.  A path cost is at most C + P2 (SGM.cpp:
+    // 93-117: L = min(...) + C - minLp <= P2 + C), C at most 999999 (the sky
+    // override, Solver.cpp:167-176), so min <= 8 (P2 + 999999); a ratio above
+    // that / FLT_MAX can never see the stale index, which this build's WTA
+    // does not keep.  Ratios at or below it (0 and negatives included) are
+    // rejected.
+    if (!(p->uniqueness > 0.0f) ||
+        (double)p->uniqueness * FLT_MAX <= 8.0 * ((double)p->p2 + 999999.0)) {
+        snprintf(why, n, "uniqueness must be > 8*(p2 + 999999)/FLT_MAX (SGM.cpp:392-408 would read "
+                         "the previous pixel's sec_min_d)");
+        return false;
+    }
     if (p->view != SGM_VIEW_LEFT && p->view != SGM_VIEW_RIGHT) {
         snprintf(why, n, "view must be SGM_VIEW_LEFT or SGM_VIEW_RIGHT");
         return false;
@@ -209,7 +218,7 @@ int dalloc(sgm_handle *h, T **p, size_t count) {
 void free_all(sgm_handle *h) {
     for (int v = 0; v < 2; ++v) {
         (void)hipFree(h->d_in[v]); (void)hipFree(h->d_sky[v]); (void)hipFree(h->d_ct[v]);
-        (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c_base[v]); (void)hipFree(h->d_s[v]);
+        (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
         for (auto &c : h->d_carry[v]) (void)hipFree(c);
         (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
     }
@@ -717,6 +726,15 @@ void pack_rows(uint8_t *dst, const uint8_t *src, size_t row_bytes, int rows, siz
 // lk_refine(..., staged = true) to read.
 int post_filter(sgm_handle *h, float *d_map, int pitch, hipStream_t st, bool to_lk) {
     const Geom g = h->g;
+    // The number of median-fill launches depends on a counter read back to
+    // the host each round; under stream capture that copy never runs, so a
+    // captured graph would replay a fixed, possibly unconverged, fill.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(h, hipStreamIsCapturing(st, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        return set_err(h, SGM_ERR_INVALID_ARG,
+                       "post_filter cannot be captured into a HIP graph (its median-fill launch "
+                       "count is read back to the host); capture frames with post_filter = 0");
     const double dnpx = (double)g.H * g.W;
     float *F = h->d_pf_work;
     HIPCHK(h, timed(h, "post_prep", dnpx, st, [&] {
@@ -862,16 +880,15 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if ((rc = dalloc(h, &h->d_ct[v], npx))) break;
         }
         for (int v = 0; v < (p->aux_only ? 0 : h->nviews) && !rc; ++v) {
-            // the final pass addresses T chunks from their top row, which for
-            // the partial last chunk lies up to K-1 rows above row 0
-            // and the row-walking passes prefetch up to PF positions past the
-            // end of the last row of C (never consumed): both volumes carry
-            // both guards
+            // the final pass addresses T (which reuses d_ch) in chunks from
+            // their top row, which for the partial last chunk lies up to K-1
+            // rows above row 0: d_ch carries that guard in front; the
+            // row-walking passes prefetch up to PF positions past the end of
+            // the last row of C (never consumed): both carry kVolGuard behind
             const size_t guard = (size_t)sgm::t_guard_rows(h->g.D) * h->g.W * h->g.D;
             if ((rc = dalloc(h, &h->d_ch_base[v], guard + nvol + sgm::kVolGuard))) break;
             h->d_ch[v] = h->d_ch_base[v] + guard;
-            if ((rc = dalloc(h, &h->d_c_base[v], guard + nvol + sgm::kVolGuard))) break;
-            h->d_c[v] = h->d_c_base[v] + guard;
+            if ((rc = dalloc(h, &h->d_c[v], nvol + sgm::kVolGuard))) break;
             if ((rc = dalloc(h, &h->d_s[v], nvol))) break;
             if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
             if ((rc = dalloc(h, &h->d_sub[v], npx))) break;

@@ -72,6 +72,10 @@ def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], ma
     shard is empty (fewer pairs than ranks) sends a zero stack without
     computing a frame, so the gather's buffers agree on every rank.
 
+    The maps `compute` returns must have been produced on torch's current
+    stream (see PipelinedGather): the staging copy and the gather are
+    ordered after that stream only.
+
     Failures are agreed on before any gather: if `compute` raises or returns
     a map of the wrong shape on any rank, every rank raises (a rank that
     raised alone would leave the others blocked in the gather)."""
@@ -111,9 +115,16 @@ class PipelinedGather:
     depth 2 the gather of step k runs under the kernels of step k+1.
 
     With gloo and device maps (tests: several ranks sharing one GPU) each
-    submit first copies the map to a host buffer (a synchronous copy, so the
-    map's producer has finished) and gathers that; `gathered()` then returns
-    host tensors."""
+    submit first copies the map to a host buffer and gathers that;
+    `gathered()` then returns host tensors.
+
+    Stream ordering: the gather (and the gloo path's host copy) is ordered
+    after the map's producer only if that producer ran on torch's CURRENT
+    stream.  Enqueue the frame with `process_device(..., stream=
+    torch.cuda.current_stream().cuda_stream)`, or make the handle's own stream
+    current (`torch.cuda.set_stream(torch.cuda.ExternalStream(sgm.stream))`,
+    as bench.py does).  `process_device(stream=None)` alone runs on the
+    handle's non-blocking stream, which torch's streams do not wait for."""
 
     def __init__(self, shape, dtype, device, depth: int = 2, group=None):
         self.group = group

@@ -73,7 +73,12 @@ def test_invalid_arguments_rejected(lib, h, w, s, d):
                                     {"view": 2}, {"view": 1},                      # views == 2
                                     {"view": 1, "views": 1, "post_filter": 1},
                                     {"view": 1, "views": 1, "lk_refine": 1},
-                                    {"view": 1, "views": 1, "solver": 1}])
+                                    {"view": 1, "views": 1, "solver": 1},
+                                    # uniqueness ratios at which SGM.cpp:392-408 reads the
+                                    # previous pixel's sec_min_d: 0, negative,
+                                    # below 8 (P2 + 999999) / FLT_MAX
+                                    {"uniqueness": 0.0}, {"uniqueness": -0.5},
+                                    {"uniqueness": 1e-33}, {"uniqueness": float("nan")}])
 def test_invalid_stage_parameters_rejected(lib, fields):
     # parameters of the section-8f stages and of the view split are checked
     # at sgm_create, before any device work (sky detector limits: sgm_sky.hip)

@@ -6,7 +6,10 @@ carrying HIP-computed disparity maps, on the one-GPU box:
   overlapped per-step gather) -- the code config 4 runs on 8 GPUs;
 * two gloo ranks sharing cuda:0 with CUDA maps: process_batch over an uneven
   batch (maps staged through the host) and the staged PipelinedGather;
-* bench.py itself under torch.distributed.run (world 1, nccl).
+* bench.py itself under torch.distributed.run (world 1, nccl);
+* config 4's batch of 8 K128 pairs on 8 gloo ranks sharing cuda:0, through
+  process_batch and the batched PipelinedGather, every map bit-equal to the
+  oracle's map for its pair.
 
 Every gathered map must equal the map a single handle computes for that pair,
 bit for bit.  Each case runs in fresh child processes (torch's HIP runtime
@@ -121,6 +124,107 @@ sgm.close()
 dist.barrier()
 dist.destroy_process_group()
 """
+
+
+# BASELINE.json configs[3] ("config 4"): a batch of 8 KITTI pairs sharded one
+# per rank over 8 ranks, maps gathered to rank 0 (node.cpp:49,93 is the
+# per-pair call each rank makes).  The box has one GPU, so the 8 ranks share
+# cuda:0 on gloo (maps staged through the host); each holds its own SGM
+# handle.  Rank 0 saves what it gathered; the test compares every map with the
+# oracle's map for that pair.
+CONFIG4 = r"""
+import os, sys, numpy as np, torch, torch.distributed as dist
+root, port, rank, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+sys.path.insert(0, root)
+from stereo_matching_amd import SGM, synthetic
+from stereo_matching_amd import distributed as sd
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+H, W, D, N, GK = 375, 1242, 128, 8, 4
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + port, rank=rank, world_size=N)
+PAIRS = [synthetic.stereo_pair(H, W, D, pair_index=i) for i in range(N)]
+stream = torch.cuda.current_stream(dev)
+sgm = SGM(H, W, 1, D, views=1, device=0)
+def compute(pair):
+    l, r = (torch.from_numpy(a).to(dev) for a in pair)
+    m = torch.empty((H, W), dtype=torch.float32, device=dev)
+    sgm.process_device(l.data_ptr(), r.data_ptr(), m.data_ptr(), stream=stream.cuda_stream)
+    return m
+batch = sd.process_batch(PAIRS, compute, (H, W))
+# bench.py's batched gather (--gather-every 4): step k of rank r computes pair
+# (k + r) % 8 into slot k % 4 of the rotating (4, H, W) buffer; one gather per
+# 4 steps, overlapped with the next 4
+pipe = sd.PipelinedGather((GK, H, W), torch.float32, dev, depth=2)
+dl = [torch.from_numpy(p[0]).to(dev) for p in PAIRS]
+dr = [torch.from_numpy(p[1]).to(dev) for p in PAIRS]
+got = {}
+for k in range(3 * GK):
+    if k % GK == 0:
+        buf = pipe.buffer()
+        if k >= 2 * GK and rank == 0:
+            got[k // GK - 2] = [t.clone() for t in pipe.gathered(k // GK - 2)]
+    p = (k + rank) % N
+    sgm.process_device(dl[p].data_ptr(), dr[p].data_ptr(), buf[k % GK].data_ptr(),
+                       stream=stream.cuda_stream)
+    if k % GK == GK - 1:
+        pipe.submit()
+pipe.drain()
+if rank == 0:
+    for b in (1, 2):
+        got[b] = [t.clone() for t in pipe.gathered(b)]
+    assert batch.device.type == "cpu" and tuple(batch.shape) == (N, H, W)
+    # pipe[b][r][s]: step b*GK + s of rank r
+    pipe_maps = np.stack([np.stack([t.numpy() for t in got[b]]) for b in range(3)])
+    np.savez(out, batch=batch.numpy(), pipe=pipe_maps)
+    print("config4 rank0 saved", flush=True)
+else:
+    assert batch is None
+sgm.close()
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.timeout(900)
+def test_config4_batch_of_8_on_the_hip_path(tmp_path):
+    import numpy as np
+
+    import oracle
+    from stereo_matching_amd import synthetic
+    oracle.build()
+    H, W, D, N, GK = 375, 1242, 128, 8, 4
+    out = str(tmp_path / "config4.npz")
+    port = _port()
+    procs = [subprocess.Popen([sys.executable, "-c", CONFIG4, ROOT, port, str(r), out],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(N)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=420))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, (so, se)) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, (r, so[-2000:] + se[-4000:])
+    assert "config4 rank0 saved" in outs[0][0]
+    res = np.load(out)
+    batch, pipe = res["batch"], res["pipe"]
+    assert batch.shape == (N, H, W) and pipe.shape == (3, N, GK, H, W)
+    for i in range(N):
+        left, right = synthetic.stereo_pair(H, W, D, pair_index=i)
+        want = oracle.process(left, right, D, views=1)["sub"].view(np.uint32)
+        assert np.array_equal(batch[i].view(np.uint32), want), ("process_batch", i)
+        # every (step, rank) that computed pair i: (b*GK + s + r) % N == i
+        hits = 0
+        for b in range(3):
+            for r in range(N):
+                for s in range(GK):
+                    if (b * GK + s + r) % N == i:
+                        assert np.array_equal(pipe[b, r, s].view(np.uint32), want), ("pipe", b, r, s)
+                        hits += 1
+        assert hits == 3 * GK
 
 
 def _port():

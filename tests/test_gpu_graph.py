@@ -54,3 +54,37 @@ def test_frame_replays_from_a_hip_graph(h, w, D, views, sky):
             torch.cuda.synchronize(dev)
             g, e = out_g.cpu().numpy(), out_e.cpu().numpy()
             assert np.array_equal(g.view(np.uint32), e.view(np.uint32)), k
+
+
+@pytest.mark.timeout(120)
+def test_capture_with_post_filter_is_rejected():
+    # post_filter's median-fill launch count comes from a counter read back to
+    # the host each round, which a capture never runs: the library refuses
+    # the capture instead of recording a fixed fill, and the
+    # handle keeps working eagerly afterwards
+    from stereo_matching_amd import SGMError
+    import oracle
+    h, w, D = 96, 320, 64
+    dev = torch.device("cuda", 0)
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=0)
+    with SGM(h, w, 1, D, views=2, post_filter=True) as sgm:
+        stream = torch.cuda.ExternalStream(sgm.stream, device=dev)
+        d_l = torch.from_numpy(left).to(dev)
+        d_r = torch.from_numpy(right).to(dev)
+        out = torch.empty((h, w), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)
+
+        def frame():
+            sgm.process_device(d_l.data_ptr(), d_r.data_ptr(), out.data_ptr(),
+                               stream=stream.cuda_stream)
+
+        graph = torch.cuda.CUDAGraph()
+        with pytest.raises(SGMError, match="HIP graph"):
+            with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+                frame()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.stream(stream):
+            frame()
+        torch.cuda.synchronize(dev)
+        want = oracle.process(left, right, D)["final"]
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
