@@ -1051,7 +1051,9 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
 // a.band.ke) only, the filter's running sum, its last output and the L3 state
 // entering the band read from a.band.carry (3 D-vectors per column) and the
 // state leaving it written back there.
-template <int V, bool FULL, int WIN, int PF, bool BAND = false>
+// L3OUT (the slanted schedule, sgm_slant.hip): every row's L3 goes to a.out
+// (a full HWD volume, streamed) instead of checkpoints.
+template <int V, bool FULL, int WIN, int PF, bool BAND = false, bool L3OUT = false>
 __device__ __forceinline__ void vfwd_body(const float *__restrict__ in, float *__restrict__ out,
                                           const PairArgs &a, const Geom &g, int j, int lane) {
     constexpr int K = pair_kv<V>();
@@ -1139,7 +1141,9 @@ __device__ __forceinline__ void vfwd_body(const float *__restrict__ in, float *_
         float L[V];
         dp_step<V>(prev, pmin, c, L, a.p1, p2v);
         const float nmin = wave_min(lane_min(L));
-        if (i == next_ck && ck_i < nseg - 1) {
+        if constexpr (L3OUT) {
+            store_v_nt<V>(a.out + (size_t)j * g.D + e0 + (size_t)i * stride, L, active);
+        } else if (i == next_ck && ck_i < nseg - 1) {
             store_v<V>(ck + (size_t)ck_i * g.D, L, active);
             ++ck_i;
             next_ck += K;

@@ -55,6 +55,11 @@ struct sgm_handle {
     float *d_zero;        // 256 zero floats (PairArgs::zero)
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
     float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
+    bool slant;           // the slanted-tile schedule (sgm_slant.hip, DESIGN.md "Slanted tiles")
+    float *d_l3[2];       // slant: the full L3 volume per view
+    unsigned long long *d_gran;  // slant: hand-off granules (both views)
+    sgm::SlantCtl *d_slant_ctl;  // slant: launch bookkeeping of the passes
+    float *d_slant_dummy;        // slant: the target of inactive lanes' stores
     int band_rows;        // rows per band of the backward phase (0: whole volume)
     bool fwd_bands;       // frames also run vfwd and stage A's diagonal roles in bands
     bool sub_cm;          // two-view frames: column-major sub-pixel maps + lr_cm_kernel
@@ -220,9 +225,13 @@ void free_all(sgm_handle *h) {
         (void)hipFree(h->d_in[v]); (void)hipFree(h->d_sky[v]); (void)hipFree(h->d_ct[v]);
         (void)hipFree(h->d_ch_base[v]); (void)hipFree(h->d_c[v]); (void)hipFree(h->d_s[v]);
         for (auto &c : h->d_carry[v]) (void)hipFree(c);
+        (void)hipFree(h->d_l3[v]);
         (void)hipFree(h->d_disp[v]); (void)hipFree(h->d_sub[v]);
     }
     (void)hipFree(h->d_out);
+    (void)hipFree(h->d_gran);
+    (void)hipFree(h->d_slant_ctl);
+    (void)hipFree(h->d_slant_dummy);
     (void)hipFree(h->d_pf_orig); (void)hipFree(h->d_pf_work); (void)hipFree(h->d_pf_label);
     (void)hipFree(h->d_pf_count); (void)hipFree(h->d_pf_area); (void)hipFree(h->d_pf_snap);
     (void)hipFree(h->d_pf_changes);
@@ -561,6 +570,58 @@ int bm_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int p
     return SGM_OK;
 }
 
+int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+                 float *d_out, int out_pitch, hipStream_t st);
+
+// The slanted-tile schedule of the aggregation (DESIGN.md "Slanted tiles"),
+// after the cost stage left each view's horizontally filtered volume in d_ch:
+//   vfwd_l3:  vertical IIR -> C, and the full L3 volume
+//   L5 -> T, T += L6 (T56 = L5 + L6, SGM.cpp:389's first association)
+//   H pair (both views): S12 = L1 + L2
+//   slant_up (both views): L4, L7, L8 walking up, total
+//     ((S12 + L3) + L4) + ((T56 + L7) + L8), WTA, sub-pixel (row-major maps)
+int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
+    const Geom g = h->g;
+    const int nv = h->nviews;
+    const double elems = (double)g.H * g.W * g.D;
+    sgm::PairArgs hp1[2], hp2[2];
+    for (int v = 0; v < nv; ++v) {
+        const sgm::PairArgs pa = pair_args(h);
+        HIPCHK(h, timed(h, "vfwd_l3", elems, st, [&] {
+                   return sgm::launch_vfwd_l3(h->d_ch[v], h->d_c[v], h->d_l3[v], pa, g, st);
+               }));
+        SweepArgs l5 = sweep_args(h);
+        l5.cost = h->d_c[v];
+        l5.acc_out = t_buf(h, v);
+        HIPCHK(h, timed(h, "sweep_L5_init", elems, st,
+                        [&] { return sgm::launch_sweep(SGM_DIR_L5, sgm::SWEEP_INIT, l5, g, st); }));
+        SweepArgs l6 = l5;
+        l6.acc_in = t_buf(h, v);
+        HIPCHK(h, timed(h, "sweep_L6_acc", elems, st,
+                        [&] { return sgm::launch_sweep(SGM_DIR_L6, sgm::SWEEP_ACC, l6, g, st); }));
+        hp1[v] = pair_args(h);
+        hp1[v].cost = h->d_c[v];
+        hp1[v].ckpt = h->d_ck[v][sgm::PAIR_H];
+        hp2[v] = hp1[v];
+        hp2[v].out = h->d_s[v];
+    }
+    HIPCHK(h, timed(h, "stage_a_h", nv * elems, st,
+                    [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, st); }));
+    sgm::SlantArgs sa{};
+    for (int v = 0; v < nv; ++v)
+        sa.v[v] = {h->d_c[v], h->d_s[v], h->d_l3[v], t_buf(h, v), v ? h->d_sub[1] : sub0,
+                   v ? nullptr : raw, h->d_gran};
+    sa.ctl = h->d_slant_ctl;
+    sa.zero = h->d_zero;
+    sa.dummy = h->d_slant_dummy;
+    sa.p1 = (float)h->p.p1;
+    sa.p2 = (float)h->p.p2;
+    sa.uniq = h->p.uniqueness;
+    sa.nviews = nv;
+    HIPCHK(h, timed(h, "slant_up", nv * elems, st, [&] { return sgm::launch_slant_up(sa, g, st); }));
+    return SGM_OK;
+}
+
 int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
               const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch, float *d_out,
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
@@ -599,8 +660,9 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     const bool both_h = h->nviews == 2 && aux1 == st && (d_sky_l == nullptr) == (d_sky_r == nullptr) &&
                         sgm::cost_h2_supported(g, d_sky_l != nullptr);
     if (h->nviews == 2 && !both_h && aux1 != st) HIPCHK(h, hipEventRecord(h->ev_ct, st));
-    // banded frames run vfwd in forward bands inside aggregate_view
-    const bool fwd_bands = h->fwd_bands;
+    // banded frames run vfwd in forward bands inside aggregate_view; the
+    // slanted schedule runs its own vertical pass
+    const bool fwd_bands = h->fwd_bands || h->slant;
     if (both_h) {
         HIPCHK(h, timed(h, "cost_h", 2.0 * npx * g.D, st, [&] {
                    return sgm::launch_cost_h2(h->d_ct[0], h->d_ct[1], d_sky_l, d_sky_r, sky_pitch, g,
@@ -629,10 +691,24 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // one view with a dense output map: the final pass writes the sub-pixel
     // map straight into it (no device copy after the frame)
     const bool direct_out = h->nviews == 1 && out_pitch == g.W;
+    float *sub0 = direct_out ? d_out : h->d_sub[0];
+    if (h->slant) {
+        if ((rc = slant_views(h, sub0, d_raw, st)) != SGM_OK) return rc;
+        if (h->nviews == 2) {
+            HIPCHK(h, timed(h, "lr", npx, st, [&] {
+                       return sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
+                                             h->p.lr_max_diff, g, st);
+                   }));
+        } else if (!direct_out) {
+            HIPCHK(h, hipMemcpy2DAsync(d_out, (size_t)out_pitch * sizeof(float), h->d_sub[0],
+                                       (size_t)g.W * sizeof(float), (size_t)g.W * sizeof(float), g.H,
+                                       hipMemcpyDeviceToDevice, st));
+        }
+        return finish_frame(h, d_left, d_right, pitch, d_out, out_pitch, st);
+    }
     // banded frames with two views on one stream: both views' forward bands,
     // then both H pairs in one launch, then each view's backward bands
     const bool split_h = fwd_bands && h->nviews == 2 && aux1 == st;
-    float *sub0 = direct_out ? d_out : h->d_sub[0];
     if (split_h) {
         sgm::PairArgs hp[2][2];
         for (int v = 0; v < 2; ++v)
@@ -676,6 +752,13 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     }
     // (the raw WTA map, when asked for, was written straight into d_raw by the
     // left view's final pass; the right view's is never written)
+    return finish_frame(h, d_left, d_right, pitch, d_out, out_pitch, st);
+}
+
+// post_filter and LKRefine at the end of a frame (SGM.cpp:821-824)
+int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
+                 float *d_out, int out_pitch, hipStream_t st) {
+    int rc;
     // with LKRefine next, the post filter's last kernel writes LKRefine's
     // input copy instead of the map (no device copy in between)
     const bool pf_to_lk = h->p.post_filter && h->p.lk_refine;
@@ -897,6 +980,22 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             // slot 2 also holds vfwd's forward-band state (3 D-vectors per column)
             for (int f = 0; f < 3 && !rc; ++f)
                 rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D * (f == 2 ? 3 : 1));
+        }
+        {
+            // the slanted schedule: SGM_SLANT=1/0 forces it on/off (parity
+            // tests cover it at every size); default off until measured
+            const char *e = getenv("SGM_SLANT");
+            h->slant = !p->aux_only && p->solver == SGM_SOLVER_SGM && e && *e == '1';
+        }
+        if (!rc && h->slant) {
+            for (int v = 0; v < h->nviews && !rc; ++v) rc = dalloc(h, &h->d_l3[v], nvol);
+            const size_t ng = sgm::slant_gran_count(h->g, h->nviews);
+            if (!rc) rc = dalloc(h, &h->d_gran, ng);
+            if (!rc) rc = dalloc(h, &h->d_slant_ctl, 2);
+            if (!rc) rc = dalloc(h, &h->d_slant_dummy, 64);
+            if (!rc && (hipMemset(h->d_gran, 0, ng * sizeof(unsigned long long)) != hipSuccess ||
+                        hipMemset(h->d_slant_ctl, 0, 2 * sizeof(sgm::SlantCtl)) != hipSuccess))
+                rc = set_err(h, SGM_ERR_HIP, "hipMemset of the slanted schedule's hand-off state failed");
         }
         h->band_rows = band_rows_for(h->g);
         {

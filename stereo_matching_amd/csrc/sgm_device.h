@@ -371,6 +371,23 @@ __device__ __forceinline__ void dp_step(const float (&prev)[V], float pmin, cons
     }
 }
 
+// x[d] of a wave-spread vector (lane d / V, slot d % V) for a wave-uniform d:
+// V readlanes and scalar selects.  (A select chain on the slot in VALU
+// registers, pick() below, is lowered by hipcc to a dynamically indexed
+// private array: scratch stores and loads, whose vmcnt waits then also wait
+// for every prefetch load in flight.)
+template <int V>
+__device__ __forceinline__ float wave_pick(const float (&x)[V], int d) {
+    const int l = d / V, v = d - l * V;
+    float r = readlane_f(x[0], l);
+#pragma unroll
+    for (int k = 1; k < V; ++k) {
+        const float t = readlane_f(x[k], l);
+        r = v == k ? t : r;
+    }
+    return r;
+}
+
 template <int V>
 __device__ __forceinline__ float pick(const float (&x)[V], int v) {
     float r = x[0];
@@ -419,9 +436,9 @@ __device__ __forceinline__ void wta_subpixel(const float (&tot)[V], int D, float
     } else if (d == 0 || d == D - 1) {
         f = (float)d;
     } else {
-        const float a = readlane_f(pick(tot, (d - 1) % V), (d - 1) / V);
-        const float b = readlane_f(pick(tot, (d + 1) % V), (d + 1) / V);
-        const float c = readlane_f(pick(tot, d % V), d / V);
+        const float a = wave_pick<V>(tot, d - 1);
+        const float b = wave_pick<V>(tot, d + 1);
+        const float c = wave_pick<V>(tot, d);
         const float x = d + (a - b) / (2 * (a + b - 2 * c));
         const float lim = (D - 1) * 1.f;
         f = (lim < x) ? lim : x;  // std::min(x, lim)

@@ -121,6 +121,41 @@ hipError_t launch_stage_a_hpair(const PairArgs *h1, const PairArgs *h2, int nvie
                                 hipStream_t st);
 hipError_t launch_stage_a_band(const SweepArgs &l5, const PairArgs &d6, Geom g, hipStream_t st);
 hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st);
+// the same vertical IIR + L3, writing every row's L3 to the volume l3 (the
+// slanted schedule's bottom-up pass reads it) instead of checkpoints
+hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs &a, Geom g,
+                          hipStream_t st);
+
+// ----------------------------------------------- slanted tiles (sgm_slant.hip)
+// Compute waves per tile (one more wave per workgroup carries the hand-offs).
+constexpr int kSlantNW = 15;
+// Launch bookkeeping of one slanted pass kind, in device memory (zeroed at
+// create): tickets claim tiles, the last workgroup out resets tickets/exits
+// and advances epoch (the hand-off granules' tag), err counts hang-guard
+// give-ups.
+struct SlantCtl {
+    unsigned tickets, exits, epoch, err;
+};
+struct SlantView {
+    const float *cost, *s12, *l3, *t56;  // HWD: C, L1+L2, L3, L5+L6
+    float *sub;                          // HW sub-pixel map, row-major
+    uint16_t *disp;                      // HW raw WTA map (null: not wanted)
+    unsigned long long *gran;            // hand-off granules, slant_gran_count
+};
+struct SlantArgs {
+    SlantView v[2];
+    SlantCtl *ctl;
+    const float *zero;  // >= 256 zero floats
+    float *dummy;       // >= 2 words: the target of inactive lanes' stores
+    float p1, p2, uniq;
+    int nviews;
+    int ntiles, grid;   // set by the launcher
+};
+size_t slant_tiles(Geom g);
+// granules (8 B each) of nviews views' hand-offs
+size_t slant_gran_count(Geom g, int nviews);
+// both views' (a.nviews) bottom-up slanted pass: L4 + L7 + L8 + WTA
+hipError_t launch_slant_up(const SlantArgs &a, Geom g, hipStream_t st);
 
 // bm_rows: BM.cpp:24-25 decimation (rows not strided by the scale); src2/ct2:
 // a second image censused in the same launch

@@ -34,10 +34,10 @@ size_t pair_ckpt_floats(int family, Geom g) {
 
 // vfwd_body (sgm_bodies.h): the vertical IIR fused with the L3 forward pass,
 // one wave per column.
-template <int V, bool FULL, int WIN, int PF, bool BAND = false>
+template <int V, bool FULL, int WIN, int PF, bool BAND = false, bool L3OUT = false>
 __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
                                                   float *__restrict__ out, PairArgs a, Geom g) {
-    vfwd_body<V, FULL, WIN, PF, BAND>(in, out, a, g, bid_x(), tid_x());
+    vfwd_body<V, FULL, WIN, PF, BAND, L3OUT>(in, out, a, g, bid_x(), tid_x());
 }
 
 template <int FD, int V, bool FULL, int PF>
@@ -236,19 +236,28 @@ hipError_t launch_pair_fwd(int family, const PairArgs &a, Geom g, hipStream_t st
     return hipGetLastError();
 }
 
-template <int WIN, bool BAND>
+template <int WIN, bool BAND, bool L3OUT = false>
 static void launch_vfwd_t(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(g.W);
-    if (g.D == 32) vfwd_kernel<1, false, WIN, 16, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
-    else if (g.D == 64) vfwd_kernel<1, true, WIN, 16, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
-    else if (g.D == 128) vfwd_kernel<2, true, WIN, 16, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
-    else vfwd_kernel<4, true, WIN, 8, BAND><<<grid, 64, 0, st>>>(in, out, a, g);
+    if (g.D == 32) vfwd_kernel<1, false, WIN, 16, BAND, L3OUT><<<grid, 64, 0, st>>>(in, out, a, g);
+    else if (g.D == 64) vfwd_kernel<1, true, WIN, 16, BAND, L3OUT><<<grid, 64, 0, st>>>(in, out, a, g);
+    else if (g.D == 128) vfwd_kernel<2, true, WIN, 16, BAND, L3OUT><<<grid, 64, 0, st>>>(in, out, a, g);
+    else vfwd_kernel<4, true, WIN, 8, BAND, L3OUT><<<grid, 64, 0, st>>>(in, out, a, g);
 }
 
 hipError_t launch_vfwd(const float *in, float *out, const PairArgs &a, Geom g, hipStream_t st) {
     const bool band = a.band.ke > 0;
     if (g.scale == 1) band ? launch_vfwd_t<3, true>(in, out, a, g, st) : launch_vfwd_t<3, false>(in, out, a, g, st);
     else band ? launch_vfwd_t<1, true>(in, out, a, g, st) : launch_vfwd_t<1, false>(in, out, a, g, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs &a, Geom g,
+                          hipStream_t st) {
+    PairArgs b = a;
+    b.out = l3;
+    if (g.scale == 1) launch_vfwd_t<3, false, true>(in, out, b, g, st);
+    else launch_vfwd_t<1, false, true>(in, out, b, g, st);
     return hipGetLastError();
 }
 

@@ -87,3 +87,16 @@ def _check(c):
     want_map = ref["lr"] if c["views"] == 2 else ref["sub"]
     assert np.array_equal(got_raw.astype(np.int64), ref["disp"].astype(np.int64)), "WTA"
     assert np.array_equal(got_map.view(np.uint32), want_map.view(np.uint32)), "map"
+
+
+@pytest.mark.parametrize("c", CASES, ids=[f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_V{c['views']}" for c in CASES])
+@pytest.mark.parametrize("split", ["0", "1"], ids=["onewave", "split"])
+def test_random_frame_slant(c, split, monkeypatch):
+    """The slanted-tile schedule (sgm_slant.hip, DESIGN.md "Slanted tiles"):
+    vfwd writing the full L3 volume, T56 = L5 + L6 by two sweeps, the H pair,
+    then one bottom-up pass of 15-column tiles leaning along L7 that runs L4,
+    L7 and L8 together, handing states to the next tile through tagged
+    granules, and the WTA."""
+    monkeypatch.setenv("SGM_SLANT", "1")
+    monkeypatch.setenv("SGM_SWEEP_SPLIT", split)
+    _check(c)
