@@ -509,6 +509,52 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     return SGM_OK;
 }
 
+// Both views' aggregation as joint launches (grid.y = view): stage A, stage
+// B, the L8 sweep and the final pass each take both views at once.  For frames
+// whose two cost volumes fit the 256 MB Infinity Cache together (K64: 2 x 119
+// MB), where one view's launches hold too few chains to fill the chip (the
+// reference runs the views back to back, SGM.cpp:32-801; the results are the
+// same per view).
+int aggregate_joint(sgm_handle *h, float *sub0, uint16_t *raw, int cm, hipStream_t st) {
+    const double elems2 = 2.0 * h->g.H * h->g.W * h->g.D;
+    sgm::PairArgs h1[2], d6[2], h2[2], d7[2], fin[2];
+    SweepArgs l5[2], l8[2];
+    for (int v = 0; v < 2; ++v) {
+        float **ck = h->d_ck[v];
+        sgm::PairArgs pa = pair_args(h);
+        pa.cost = cost_buf(h, v);
+        h1[v] = pa;
+        h1[v].ckpt = ck[sgm::PAIR_H];
+        d6[v] = pa;
+        d6[v].ckpt = ck[sgm::PAIR_D2];
+        h2[v] = h1[v];
+        h2[v].out = h->d_s[v];
+        d7[v] = d6[v];
+        d7[v].acc_in = t_buf(h, v);
+        d7[v].out = t_buf(h, v);
+        l5[v] = sweep_args(h);
+        l5[v].cost = cost_buf(h, v);
+        l5[v].acc_out = t_buf(h, v);
+        l8[v] = l5[v];
+        l8[v].acc_in = t_buf(h, v);
+        fin[v] = pa;
+        fin[v].ckpt = ck[sgm::PAIR_V];
+        fin[v].s_in = h->d_s[v];
+        fin[v].acc_in = t_buf(h, v);
+        fin[v].disp = v ? nullptr : raw;
+        fin[v].sub = v ? h->d_sub[1] : sub0;
+        fin[v].sub_cm = cm;
+    }
+    const Geom g = h->g;
+    HIPCHK(h, timed(h, "stage_a", elems2, st, [&] { return sgm::launch_stage_a2(h1, l5, d6, g, st); }));
+    HIPCHK(h, timed(h, "stage_b", elems2, st, [&] { return sgm::launch_stage_b2(h2, d7, g, st); }));
+    HIPCHK(h, timed(h, "sweep_L8_acc", elems2, st,
+                    [&] { return sgm::launch_sweep2_l8(l8[0], l8[1], g, st); }));
+    HIPCHK(h, timed(h, "pair_bwd_L4_final", elems2, st,
+                    [&] { return sgm::launch_final2(fin[0], fin[1], g, st); }));
+    return SGM_OK;
+}
+
 // build_dsi_from_table[_beta] (dsi 0 / 1) + horizontal IIR (cost_h), then
 // the vertical IIR fused with the L3 forward pass (vfwd), into view slot
 // `view`'s buffers.
@@ -575,8 +621,9 @@ int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, i
 
 // The slanted-tile schedule of the aggregation (DESIGN.md "Slanted tiles"),
 // after the cost stage left each view's horizontally filtered volume in d_ch:
-//   vfwd_l3:  vertical IIR -> C, and the full L3 volume
-//   L5 -> T, T += L6 (T56 = L5 + L6, SGM.cpp:389's first association)
+//   vfwd_l3 (per view): vertical IIR -> C, and the full L3 volume
+//   slant_down (both views): T56 = L5 + L6 (SGM.cpp:389's first association)
+//     into the dead horizontally filtered volume
 //   H pair (both views): S12 = L1 + L2
 //   slant_up (both views): L4, L7, L8 walking up, total
 //     ((S12 + L3) + L4) + ((T56 + L7) + L8), WTA, sub-pixel (row-major maps)
@@ -585,32 +632,20 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     const int nv = h->nviews;
     const double elems = (double)g.H * g.W * g.D;
     sgm::PairArgs hp1[2], hp2[2];
+    sgm::SlantArgs sa{};
     for (int v = 0; v < nv; ++v) {
         const sgm::PairArgs pa = pair_args(h);
         HIPCHK(h, timed(h, "vfwd_l3", elems, st, [&] {
                    return sgm::launch_vfwd_l3(h->d_ch[v], h->d_c[v], h->d_l3[v], pa, g, st);
                }));
-        SweepArgs l5 = sweep_args(h);
-        l5.cost = h->d_c[v];
-        l5.acc_out = t_buf(h, v);
-        HIPCHK(h, timed(h, "sweep_L5_init", elems, st,
-                        [&] { return sgm::launch_sweep(SGM_DIR_L5, sgm::SWEEP_INIT, l5, g, st); }));
-        SweepArgs l6 = l5;
-        l6.acc_in = t_buf(h, v);
-        HIPCHK(h, timed(h, "sweep_L6_acc", elems, st,
-                        [&] { return sgm::launch_sweep(SGM_DIR_L6, sgm::SWEEP_ACC, l6, g, st); }));
         hp1[v] = pair_args(h);
         hp1[v].cost = h->d_c[v];
         hp1[v].ckpt = h->d_ck[v][sgm::PAIR_H];
         hp2[v] = hp1[v];
         hp2[v].out = h->d_s[v];
+        sa.v[v] = {h->d_c[v], h->d_s[v], h->d_l3[v], t_buf(h, v), t_buf(h, v),
+                   v ? h->d_sub[1] : sub0, v ? nullptr : raw, h->d_gran};
     }
-    HIPCHK(h, timed(h, "stage_a_h", nv * elems, st,
-                    [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, st); }));
-    sgm::SlantArgs sa{};
-    for (int v = 0; v < nv; ++v)
-        sa.v[v] = {h->d_c[v], h->d_s[v], h->d_l3[v], t_buf(h, v), v ? h->d_sub[1] : sub0,
-                   v ? nullptr : raw, h->d_gran};
     sa.ctl = h->d_slant_ctl;
     sa.zero = h->d_zero;
     sa.dummy = h->d_slant_dummy;
@@ -618,6 +653,9 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     sa.p2 = (float)h->p.p2;
     sa.uniq = h->p.uniqueness;
     sa.nviews = nv;
+    HIPCHK(h, timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); }));
+    HIPCHK(h, timed(h, "stage_a_h", nv * elems, st,
+                    [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, st); }));
     HIPCHK(h, timed(h, "slant_up", nv * elems, st, [&] { return sgm::launch_slant_up(sa, g, st); }));
     return SGM_OK;
 }
@@ -706,6 +744,10 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         }
         return finish_frame(h, d_left, d_right, pitch, d_out, out_pitch, st);
     }
+    // two views whose cost volumes fit the Infinity Cache together: joint
+    // launches (aggregate_joint)
+    const bool joint = h->nviews == 2 && aux1 == st && h->band_rows == 0 &&
+                       2.0 * g.H * g.W * g.D * sizeof(float) <= 256.0 * 1024 * 1024;
     // banded frames with two views on one stream: both views' forward bands,
     // then both H pairs in one launch, then each view's backward bands
     const bool split_h = fwd_bands && h->nviews == 2 && aux1 == st;
@@ -724,11 +766,16 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // two views: the final passes write column-major sub-pixel maps (whole
     // cache lines; lr_cm_kernel reads them through LDS tiles)
     const int cm = h->nviews == 2 && h->sub_cm ? 1 : 0;
-    if ((rc = aggregate_view(h, 0, cost_buf(h, 0), h->d_s[0], t_buf(h, 0), d_raw, sub0, st, false,
-                             both_final ? &fin[0] : nullptr, fwd_bands, part, nullptr, cm)) != SGM_OK)
+    if (joint) {
+        if ((rc = aggregate_joint(h, sub0, d_raw, cm, st)) != SGM_OK) return rc;
+    } else if ((rc = aggregate_view(h, 0, cost_buf(h, 0), h->d_s[0], t_buf(h, 0), d_raw, sub0, st,
+                                    false, both_final ? &fin[0] : nullptr, fwd_bands, part, nullptr,
+                                    cm)) != SGM_OK) {
         return rc;
+    }
     if (h->nviews == 2) {
-        if ((rc = aggregate_view(h, 1, cost_buf(h, 1), h->d_s[1], t_buf(h, 1), nullptr, h->d_sub[1],
+        if (!joint &&
+            (rc = aggregate_view(h, 1, cost_buf(h, 1), h->d_s[1], t_buf(h, 1), nullptr, h->d_sub[1],
                                  aux1, false, both_final ? &fin[1] : nullptr, fwd_bands,
                                  part, nullptr, cm)) != SGM_OK)
             return rc;
@@ -992,7 +1039,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             const size_t ng = sgm::slant_gran_count(h->g, h->nviews);
             if (!rc) rc = dalloc(h, &h->d_gran, ng);
             if (!rc) rc = dalloc(h, &h->d_slant_ctl, 2);
-            if (!rc) rc = dalloc(h, &h->d_slant_dummy, 64);
+            if (!rc) rc = dalloc(h, &h->d_slant_dummy, 512);
             if (!rc && (hipMemset(h->d_gran, 0, ng * sizeof(unsigned long long)) != hipSuccess ||
                         hipMemset(h->d_slant_ctl, 0, 2 * sizeof(sgm::SlantCtl)) != hipSuccess))
                 rc = set_err(h, SGM_ERR_HIP, "hipMemset of the slanted schedule's hand-off state failed");
@@ -1131,6 +1178,21 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
     if (raw_disp) memcpy(raw_disp, praw, npx * sizeof(uint16_t));
     return SGM_OK;
 }
+
+#ifdef SGM_SLANT_DEBUG
+// hang-guard give-ups of the slanted passes (SlantCtl::err), read and cleared
+int sgm_debug_slant_err(sgm_handle *h, unsigned *down, unsigned *up) {
+    if (!h || !h->d_slant_ctl) return SGM_ERR_INVALID_ARG;
+    sgm::SlantCtl c[2];
+    HIPCHK(h, hipDeviceSynchronize());
+    HIPCHK(h, hipMemcpy(c, h->d_slant_ctl, sizeof(c), hipMemcpyDeviceToHost));
+    *down = c[0].err;
+    *up = c[1].err;
+    c[0].err = c[1].err = 0;
+    HIPCHK(h, hipMemcpy(h->d_slant_ctl, c, sizeof(c), hipMemcpyHostToDevice));
+    return SGM_OK;
+}
+#endif
 
 int sgm_set_profiling(sgm_handle *h, int enable) {
     if (!h) return SGM_ERR_INVALID_ARG;

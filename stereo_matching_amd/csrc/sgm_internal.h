@@ -114,6 +114,12 @@ hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStre
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
                           hipStream_t st, const PairArgs *h2 = nullptr);
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st);
+// both views' stage A / stage B / L8 sweep in one launch each (grid.y = view;
+// arrays of two)
+hipError_t launch_stage_a2(const PairArgs *h1, const SweepArgs *l5, const PairArgs *d6, Geom g,
+                           hipStream_t st);
+hipError_t launch_stage_b2(const PairArgs *h2, const PairArgs *d7, Geom g, hipStream_t st);
+hipError_t launch_sweep2_l8(const SweepArgs &a0, const SweepArgs &a1, Geom g, hipStream_t st);
 // the forward bands (DESIGN.md "Bands"): the whole H pair (L1 fwd, then L2
 // bwd -> h2[v].out) of nviews views as one launch, and one band (l5.band, d6.band)
 // of stage A's diagonal roles (L5 -> T5, L6 fwd)
@@ -137,7 +143,8 @@ struct SlantCtl {
     unsigned tickets, exits, epoch, err;
 };
 struct SlantView {
-    const float *cost, *s12, *l3, *t56;  // HWD: C, L1+L2, L3, L5+L6
+    const float *cost, *s12, *l3, *t56;  // HWD: C, L1+L2, L3, L5+L6 (bottom-up reads)
+    float *t56w;                         // HWD: L5+L6 (the top-down pass writes it)
     float *sub;                          // HW sub-pixel map, row-major
     uint16_t *disp;                      // HW raw WTA map (null: not wanted)
     unsigned long long *gran;            // hand-off granules, slant_gran_count
@@ -146,7 +153,7 @@ struct SlantArgs {
     SlantView v[2];
     SlantCtl *ctl;
     const float *zero;  // >= 256 zero floats
-    float *dummy;       // >= 2 words: the target of inactive lanes' stores
+    float *dummy;       // >= 258 words: the target of inactive steps' stores
     float p1, p2, uniq;
     int nviews;
     int ntiles, grid;   // set by the launcher
@@ -154,8 +161,10 @@ struct SlantArgs {
 size_t slant_tiles(Geom g);
 // granules (8 B each) of nviews views' hand-offs
 size_t slant_gran_count(Geom g, int nviews);
-// both views' (a.nviews) bottom-up slanted pass: L4 + L7 + L8 + WTA
+// both views' (a.nviews) bottom-up slanted pass: L4 + L7 + L8 + WTA (ctl[1])
 hipError_t launch_slant_up(const SlantArgs &a, Geom g, hipStream_t st);
+// both views' top-down slanted pass: T56 = L5 + L6 (ctl[0])
+hipError_t launch_slant_down(const SlantArgs &a, Geom g, hipStream_t st);
 
 // bm_rows: BM.cpp:24-25 decimation (rows not strided by the scale); src2/ct2:
 // a second image censused in the same launch

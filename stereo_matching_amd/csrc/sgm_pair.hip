@@ -167,6 +167,63 @@ __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, 
     if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC, !HROWS>(d7, g, path, nullptr, nullptr);
 }
 
+// Both views' stage A / stage B in one launch (workgroup y = view): frames
+// whose two cost volumes fit the 256 MB Infinity Cache together (K64), where
+// one view's launches leave most SIMDs with a single chain.
+template <int V, bool FULL>
+__global__ __launch_bounds__(64) void stage_a2_kernel(PairArgs h1a, SweepArgs l5a, PairArgs d6a,
+                                                      PairArgs h1b, SweepArgs l5b, PairArgs d6b,
+                                                      Geom g) {
+    constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
+    const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
+    int b = bid_x();
+    if (b < g.H) {
+        __builtin_amdgcn_s_setprio(3);
+        pair_fwd_body<0, V, FULL, PFH>(vb ? h1b : h1a, g, b);
+        return;
+    }
+    b -= g.H;
+    if (b < g.W) {
+        sweep_body<4, V, SWEEP_INIT, FULL, PFD>(vb ? l5b : l5a, g, b);
+        return;
+    }
+    pair_fwd_body<5, V, FULL, PFD>(vb ? d6b : d6a, g, b - g.W);
+}
+
+template <int V, bool FULL>
+__global__ __launch_bounds__(128) void stage_b2_kernel(PairArgs h2a, PairArgs d7a, PairArgs h2b,
+                                                       PairArgs d7b, Geom g) {
+    constexpr int K = pair_k<V>();
+    __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
+    const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
+    const int b = bid_x(), wave = wave_id();
+    if (b < g.H) {
+        pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K, 3>(vb ? h2b : h2a, g, b, wave, lds, nullptr);
+        return;
+    }
+    const int path = 2 * (b - g.H) + wave;
+    if (path < g.W) pair_bwd_body<PAIR_D2, V, FULL, PAIR_ACC>(vb ? d7b : d7a, g, path, nullptr, nullptr);
+}
+
+hipError_t launch_stage_a2(const PairArgs *h1, const SweepArgs *l5, const PairArgs *d6, Geom g,
+                           hipStream_t st) {
+    const dim3 grid(g.H + 2 * g.W, 2);
+    if (g.D == 32) stage_a2_kernel<1, false><<<grid, 64, 0, st>>>(h1[0], l5[0], d6[0], h1[1], l5[1], d6[1], g);
+    else if (g.D == 64) stage_a2_kernel<1, true><<<grid, 64, 0, st>>>(h1[0], l5[0], d6[0], h1[1], l5[1], d6[1], g);
+    else if (g.D == 128) stage_a2_kernel<2, true><<<grid, 64, 0, st>>>(h1[0], l5[0], d6[0], h1[1], l5[1], d6[1], g);
+    else stage_a2_kernel<4, true><<<grid, 64, 0, st>>>(h1[0], l5[0], d6[0], h1[1], l5[1], d6[1], g);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage_b2(const PairArgs *h2, const PairArgs *d7, Geom g, hipStream_t st) {
+    const dim3 grid(g.H + (g.W + 1) / 2, 2);
+    if (g.D == 32) stage_b2_kernel<1, false><<<grid, 128, 0, st>>>(h2[0], d7[0], h2[1], d7[1], g);
+    else if (g.D == 64) stage_b2_kernel<1, true><<<grid, 128, 0, st>>>(h2[0], d7[0], h2[1], d7[1], g);
+    else if (g.D == 128) stage_b2_kernel<2, true><<<grid, 128, 0, st>>>(h2[0], d7[0], h2[1], d7[1], g);
+    else stage_b2_kernel<4, true><<<grid, 128, 0, st>>>(h2[0], d7[0], h2[1], d7[1], g);
+    return hipGetLastError();
+}
+
 template <bool HP, int ROLES = 0>
 static void launch_stage_a_t(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6,
                              const PairArgs &h2, Geom g, hipStream_t st, int nblk) {

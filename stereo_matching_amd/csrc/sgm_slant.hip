@@ -15,46 +15,72 @@
 // LOWER wave numbers: L4 from wave k+1, L8 from wave k+2 of the previous
 // step.  Waves exchange them through LDS; the last one or two waves of a tile
 // take them from the next tile (t+1), whose first waves publish them as
-// 8-byte {value, tag} granules (no flag, no fence: the data is the flag,
+// 8-byte tagged granules (no flag, no fence: the data is the flag,
 // cdna_hip_programming.md Guideline 16, R2).  All dependencies point from
 // tile t+1 to tile t, so tiles claimed in the order t = T-1, T-2, ... never
 // wait on a tile no workgroup holds: no deadlock for any grid size, and a
 // tile may run any number of steps behind its right neighbour.
 //
-// The bottom-up pass (slant_up_kernel) computes, per pixel,
-//   L4 (SGM.cpp:201-239), L7, L8 (:311-369),
-//   total = ((S12 + L3) + L4) + ((T56 + L7) + L8)   (SGM.cpp:386-390)
-// and the WTA + uniqueness + sub-pixel (SGM.cpp:372-418, Solver.cpp:569-597),
-// reading C, S12 = L1+L2, L3 and T56 = L5+L6 once each (16 B per element
-// instead of the 36.75 of stage B's diagonal pair + L8 + the final pass).
+// Two passes share the kernel (slant_kernel<UP, ...>):
+//  * top-down (UP = false; tiles lean along L5, whose chains stay in a wave,
+//    L6 comes from wave k+2): T56 = L5 + L6 (SGM.cpp:247-305; the first
+//    association of SGM.cpp:389), reading C and writing T56: 8 B per element
+//    instead of the two diagonal sweeps' 20;
+//  * bottom-up (UP = true; tiles lean along L7, L4 from wave k+1, L8 from
+//    wave k+2): L4 (SGM.cpp:201-239), L7, L8 (:311-369),
+//      total = ((S12 + L3) + L4) + ((T56 + L7) + L8)   (SGM.cpp:386-390)
+//    and the WTA + uniqueness + sub-pixel (SGM.cpp:372-418, Solver.cpp:
+//    569-597), reading C, S12 = L1+L2, L3 and T56 once each: 16 B per
+//    element instead of the 36.75 of stage B's diagonal pair + L8 + the final
+//    pass.
 #include "sgm_bodies.h"
+
+#include <cstdlib>
 
 namespace sgm {
 
-// Per-step LDS exchange of one tile: the L4 and L8 states (and their minima)
-// of every wave for the previous step (parity (s-1)&1) and this one (s&1);
-// slots NW and NW+1 hold the next tile's wave 0 / wave 1 states, put there
-// by the courier wave.
-template <int V, int NW>
-struct SlantUpLds {
-    float st[2][NW + 2][2][64 * V];
-    float pm[2][NW + 2][2];
+// Per-step LDS exchange of one tile: the exchanged chain states (NE per wave:
+// bottom-up L4 and L8, top-down L6) and their minima, for the previous step
+// (parity (s-1)&1) and this one (s&1); slots NW and NW+1 hold the next tile's
+// wave 0 / wave 1 states, put there by the courier wave.
+template <int V, int NW, int NE>
+struct SlantLds {
+    float st[2][NW + 2][NE][64 * V];
+    float pm[2][NW + 2][NE];
     int ticket;
     unsigned epoch;
 };
 
-// granule index of (view, tile, step, slot 0..2, disparity): slot 0 = wave 0's
-// L4, slot 1 = wave 0's L8, slot 2 = wave 1's L8
+// granule index of (view, tile, step, slot 0..2, disparity).  Bottom-up:
+// slot 0 = wave 0's L4, 1 = wave 0's L8, 2 = wave 1's L8; top-down: 0 = wave
+// 0's L6, 1 = wave 1's L6.  The two passes share the buffer: their tags
+// differ in parity.
 __device__ __forceinline__ size_t gran_index(int T, int H, int D, int view, int t, int s, int slot) {
     return ((((size_t)view * T + t) * H + s) * 3 + slot) * D;
+}
+
+// A granule carries one float with a 16-bit tag in EACH 4-byte half:
+// {tag:16 | lo16} {tag:16 | hi16}.  An 8-byte store is observed untorn on
+// gfx950 (not an architectural guarantee, cdna_hip_programming.md Guideline
+// 16); with the tag in both halves a torn read -- one half of this launch's
+// store, one of an older one (the other pass shares the buffer) -- fails the
+// check instead of passing a value that was never written.
+__device__ __forceinline__ unsigned long long granule(float x, unsigned tag) {
+    const unsigned b = __float_as_uint(x), t = tag << 16;
+    return ((unsigned long long)(t | (b >> 16)) << 32) | (t | (b & 0xffffu));
+}
+__device__ __forceinline__ bool granule_ok(unsigned long long q, unsigned tag) {
+    return (unsigned)(q >> 48) == tag && ((unsigned)q >> 16) == tag;
+}
+__device__ __forceinline__ float granule_value(unsigned long long q) {
+    return __uint_as_float(((unsigned)(q >> 16) & 0xffff0000u) | ((unsigned)q & 0xffffu));
 }
 
 template <int V>
 __device__ __forceinline__ void store_granules(unsigned long long *g, const float (&x)[V], unsigned tag) {
 #pragma unroll
     for (int v = 0; v < V; ++v)
-        __hip_atomic_store(g + v, ((unsigned long long)tag << 32) | __float_as_uint(x[v]),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + v, granule(x[v], tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ float uni_f(float x) {
@@ -65,8 +91,7 @@ __device__ __forceinline__ float uni_f(float x) {
 // [0] tile-steps (compute wave 0)  [1] courier phases that re-polled
 // [2] courier re-polls  [3] courier cycles in re-polls  [4] compute wave 0
 // cycles between barriers  [5] compute wave 0 cycles in barriers
-// [6] courier cycles between barriers  [7] cycles inside tiles (wave 0)
-// [8] workgroups  [9] tiles
+// [7] cycles inside tiles (wave 0)  [8] workgroups  [9] tiles
 static __device__ unsigned long long slant_stamps[16];
 #define SLANT_STAMP(i, v) atomicAdd(&slant_stamps[i], (unsigned long long)(v))
 #endif
@@ -74,34 +99,52 @@ static __device__ unsigned long long slant_stamps[16];
 // polls before a courier gives up (a hang guard: ~seconds; SlantCtl::err is set)
 constexpr unsigned kSlantSpinLimit = 1u << 22;
 
+// Exit states of a tile per step, as (wave, exchanged-state index) pairs:
+// bottom-up (w0 L4, w0 L8, w1 L8), top-down (w0 L6, w1 L6).
+template <bool UP>
+struct SlantExits {
+    static constexpr int NX = UP ? 3 : 2;
+    __device__ static constexpr int wave(int e) { return UP ? (e == 2 ? 1 : 0) : e; }
+    __device__ static constexpr int kind(int e) { return UP ? (e == 0 ? 0 : 1) : 0; }
+};
+
 // PF: steps of data loads in flight per compute wave; CR: phases of hand-off
 // granule loads in flight in the courier.
 //
 // Memory-instruction hygiene (as the other passes): every
-// load and store of the steady-state loops is unconditional -- addresses are
-// clamped into the volume, inactive lanes and steps write to a dummy word --
-// so hipcc's waitcnt pass keeps exact vmcnt counts and the prefetch rings stay
-// in flight across steps (a data-dependent branch around any memory
-// instruction makes it wait for everything outstanding).
-template <int V, bool FULL, int NW, int PF, int CR>
-__global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Geom g) {
-    __shared__ __attribute__((aligned(16))) SlantUpLds<V, NW> L;
+// load and store of the steady-state loops is unconditional -- load
+// addresses are clamped into the volume, inactive steps store to a dummy
+// area -- so hipcc's waitcnt pass keeps exact vmcnt counts and the prefetch
+// rings stay in flight across steps (a branch around a memory instruction
+// makes later waits drain everything outstanding).
+template <bool UP, int V, bool FULL, int NW, int PF, int CR>
+__global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom g) {
+    constexpr int NE = UP ? 2 : 1;         // states exchanged per wave
+    constexpr int K2 = UP ? 1 : 0;         // index of the wave k+2 family (L8 / L6)
+    using X = SlantExits<UP>;
+    constexpr int NX = X::NX;
+    __shared__ __attribute__((aligned(16))) SlantLds<V, NW, NE> L;
     const int wave = wave_id(), lane = tid_x() & 63;
     const int H = g.H, W = g.W, D = g.D;
     const int e0 = lane * V;
     const bool dact = FULL || e0 < D;
     const int T = a.ntiles, total = T * a.nviews;
-    const long long dstep = (long long)(W - 1) * D;  // one step up-right: -W*D + D
+    SlantCtl *ctl = a.ctl + (UP ? 1 : 0);
+    // one step: up-right (-W*D + D) bottom-up, down-right (W*D + D) top-down
+    const long long dstep = UP ? -(long long)(W - 1) * D : (long long)(W + 1) * D;
     if (tid_x() == 0)
-        L.epoch = __hip_atomic_load(&a.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.epoch = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float p2v = to_vgpr(a.p2);
 
     for (;;) {
         __syncthreads();
-        if (tid_x() == 0) L.ticket = (int)atomicAdd(&a.ctl->tickets, 1u);
+        if (tid_x() == 0) L.ticket = (int)atomicAdd(&ctl->tickets, 1u);
         __syncthreads();
         const int r = __builtin_amdgcn_readfirstlane(L.ticket);
-        const unsigned tag = __builtin_amdgcn_readfirstlane(L.epoch) + 1u;
+        // 16-bit tags, never 0 (the zeroed buffer): 1 + (2 * epoch + pass) mod
+        // 65535, so consecutive launches and the two passes of a frame differ
+        const unsigned tag =
+            1u + (2u * __builtin_amdgcn_readfirstlane(L.epoch) + (UP ? 1u : 0u)) % 65535u;
         if (r >= total) break;
         const int view = a.nviews == 2 ? (r & 1) : 0;
         const int t = T - 1 - (a.nviews == 2 ? (r >> 1) : r);
@@ -116,7 +159,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
             // Phase p = 0 .. nsteps (the prologue, then one per step; each
             // ends on the tile's barrier):
             //  * publishes this tile's exit states of step s_begin + p - 1
-            //    (waves 0 and 1 wrote them to LDS in that step) as granules;
+            //    (its waves 0 and 1 wrote them to LDS in that step) as
+            //    granules;
             //  * hands the next tile's exit states of step gs = s_begin - 1 + p
             //    to LDS parity gs & 1 (slots NW, NW+1), which step gs + 1
             //    reads.  Their granule loads run CR phases ahead; a phase
@@ -125,58 +169,66 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
                 return t + 1 < T && (p >= 1 || s_begin >= 1) && p < nsteps;
             };
             // granules of (tile t+1, step s_begin - 1 + p); a phase with
-            // nothing to fetch loads (and ignores) tile t+1's first step, or
-            // this tile's own when t + 1 == T: every load stays in the buffer
+            // nothing to fetch loads (and ignores) this tile's first step's,
+            // so every load stays inside the buffer
             auto gsrc = [&](int p) -> const unsigned long long * {
-                const int gs = s_begin - 1 + p;
                 const bool ok = gvalid(p);
                 const int tt = uniform(ok ? t + 1 : t);
-                const int ss = uniform(ok ? gs : s_begin);
+                const int ss = uniform(ok ? s_begin - 1 + p : s_begin);
                 return sv.gran + gran_index(T, H, D, view, tt, ss, 0) + e0;
             };
-            unsigned long long rq[CR][3][V];
+            unsigned long long rq[CR][NX][V];
             auto issue = [&](int slot, int p) {
+#ifdef SLANT_PROBE_NOCOURIER
+                return;  // timing probe: no hand-off loads (wrong results)
+#endif
                 const unsigned long long *gb = gsrc(p);
 #pragma unroll
-                for (int x = 0; x < 3; ++x)
+                for (int x = 0; x < NX; ++x)
 #pragma unroll
                     for (int v = 0; v < V; ++v)
                         rq[slot][x][v] = __hip_atomic_load(const_cast<unsigned long long *>(gb + x * D + v),
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             };
+            auto publish = [&](int sp) {
+                const int par = sp & 1;
+                unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t, sp, 0) + e0;
+#pragma unroll
+                for (int x = 0; x < NX; ++x) {
+                    float y[V];
+                    load_lds_v<V>(y, &L.st[par][X::wave(x)][X::kind(x)][e0]);
+                    store_granules<V>(gb + x * D, y, tag);
+                }
+            };
 #pragma unroll
             for (int q = 0; q < CR; ++q) issue(q, q);
             auto phase = [&](int slot, int p) {
-                // 1) publish: this tile's step sp = s_begin + p - 1 (the
-                // prologue phase republishes nothing new: it rewrites step
-                // s_begin's slots, which step s_begin's phase overwrites)
-                {
-                    const int sp = uniform(p >= 1 ? s_begin + p - 1 : s_begin);
-                    const int par = sp & 1;
-                    float y0[V], y1[V], y2[V];
-                    load_lds_v<V>(y0, &L.st[par][0][0][e0]);
-                    load_lds_v<V>(y1, &L.st[par][0][1][e0]);
-                    load_lds_v<V>(y2, &L.st[par][1][1][e0]);
-                    unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t, sp, 0) + e0;
-                    if (p >= 1) {
-                        store_granules<V>(gb, y0, tag);
-                        store_granules<V>(gb + D, y1, tag);
-                        store_granules<V>(gb + 2 * D, y2, tag);
-                    }
-                }
+                // 1) publish this tile's step s_begin + p - 2, completed at the
+                // barrier that ended the previous phase (the compute waves run
+                // step s_begin + p - 1 during this phase)
+                if (p >= 2) publish(s_begin + p - 2);
                 // 2) receive tile t+1's step gs = s_begin - 1 + p
                 const int gs = s_begin - 1 + p;
                 const bool want = gvalid(p);
                 const int c0 = u_lo + NW + gs;  // tile t+1's wave 0 column at step gs
-                const bool n0 = want && c0 >= 0 && c0 < W, n1 = want && c0 + 1 >= 0 && c0 + 1 < W;
-                bool ok = true;
+                bool need[NX];
 #pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    ok &= !n0 || (unsigned)(rq[slot][0][v] >> 32) == tag;
-                    ok &= !n0 || (unsigned)(rq[slot][1][v] >> 32) == tag;
-                    ok &= !n1 || (unsigned)(rq[slot][2][v] >> 32) == tag;
+                for (int x = 0; x < NX; ++x) {
+                    const int c = c0 + X::wave(x);
+                    need[x] = want && c >= 0 && c < W;
                 }
-                if (!__all(ok || !dact)) {
+                auto check = [&] {
+                    bool ok = true;
+#pragma unroll
+                    for (int x = 0; x < NX; ++x)
+#pragma unroll
+                        for (int v = 0; v < V; ++v) ok &= !need[x] || granule_ok(rq[slot][x][v], tag);
+#if defined(SLANT_PROBE_NOWAIT) || defined(SLANT_PROBE_NOCOURIER)
+                    ok = true;  // timing probe: no hand-off wait (wrong results)
+#endif
+                    return ok || !dact;
+                };
+                if (!__all(check())) {
                     // slow path: the next tile is not CR steps ahead
 #ifdef SGM_SLANT_STAMPS
                     const long long sp0 = __builtin_amdgcn_s_memtime();
@@ -186,28 +238,18 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
                     for (unsigned spins = 1;; ++spins) {
                         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-                        for (int x = 0; x < 3; ++x)
+                        for (int x = 0; x < NX; ++x)
 #pragma unroll
                             for (int v = 0; v < V; ++v)
                                 rq[slot][x][v] = __hip_atomic_load(
                                     const_cast<unsigned long long *>(gb + x * D + v), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
-                        ok = true;
-#pragma unroll
-                        for (int v = 0; v < V; ++v) {
-                            ok &= !n0 || (unsigned)(rq[slot][0][v] >> 32) == tag;
-                            ok &= !n0 || (unsigned)(rq[slot][1][v] >> 32) == tag;
-                            ok &= !n1 || (unsigned)(rq[slot][2][v] >> 32) == tag;
-                        }
-#ifdef SLANT_PROBE_NOWAIT
-                        ok = true;  // timing probe: no hand-off wait (wrong results)
-#endif
 #ifdef SGM_SLANT_STAMPS
                         nsp = spins;
 #endif
-                        if (__all(ok || !dact)) break;
+                        if (__all(check())) break;
                         if (spins >= kSlantSpinLimit) {
-                            if (lane == 0) atomicOr(&a.ctl->err, 1u);
+                            if (lane == 0) atomicOr(&ctl->err, 1u);
                             break;
                         }
                     }
@@ -219,25 +261,17 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
                     }
 #endif
                 }
-                // (phases with nothing wanted write slots no valid
+                // (a phase with nothing wanted writes slots that no valid
                 // predecessor reads)
-                float x0[V], x1[V], x2[V];
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    x0[v] = dact ? __uint_as_float((unsigned)rq[slot][0][v]) : SGM_INF;
-                    x1[v] = dact ? __uint_as_float((unsigned)rq[slot][1][v]) : SGM_INF;
-                    x2[v] = dact ? __uint_as_float((unsigned)rq[slot][2][v]) : SGM_INF;
-                }
                 const int par = gs & 1;
-                const float m0 = wave_min(lane_min(x0)), m1 = wave_min(lane_min(x1)),
-                            m2 = wave_min(lane_min(x2));
-                store_lds_v<V>(&L.st[par][NW][0][e0], x0);
-                store_lds_v<V>(&L.st[par][NW][1][e0], x1);
-                store_lds_v<V>(&L.st[par][NW + 1][1][e0], x2);
-                if (lane == 0) {
-                    L.pm[par][NW][0] = m0;
-                    L.pm[par][NW][1] = m1;
-                    L.pm[par][NW + 1][1] = m2;
+#pragma unroll
+                for (int x = 0; x < NX; ++x) {
+                    float y[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v) y[v] = dact ? granule_value(rq[slot][x][v]) : SGM_INF;
+                    const float m = wave_min(lane_min(y));
+                    store_lds_v<V>(&L.st[par][NW + X::wave(x)][X::kind(x)][e0], y);
+                    if (lane == 0) L.pm[par][NW + X::wave(x)][X::kind(x)] = m;
                 }
                 issue(slot, p + CR);
                 lds_barrier();
@@ -251,57 +285,50 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
 #pragma unroll
             for (int q = 0; q < CR; ++q)
                 if (p0 + q < np) phase(q, p0 + q);
-            // the tile's last step, published after its barrier
-            {
-                const int sp = s_end - 1, par = sp & 1;
-                float y0[V], y1[V], y2[V];
-                load_lds_v<V>(y0, &L.st[par][0][0][e0]);
-                load_lds_v<V>(y1, &L.st[par][0][1][e0]);
-                load_lds_v<V>(y2, &L.st[par][1][1][e0]);
-                unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t, sp, 0) + e0;
-                store_granules<V>(gb, y0, tag);
-                store_granules<V>(gb + D, y1, tag);
-                store_granules<V>(gb + 2 * D, y2, tag);
-            }
+            publish(s_end - 1);  // the tile's last step, after its barrier
             continue;
         }
 
         // ------------------------------------------------- compute waves
         const int k = wave;
         const int u = u_lo + k;
-        // pixel of step s: row H-1-s, column u+s.  Steps where this wave's
-        // pixel lies outside the image load a clamped (valid) pixel and
-        // their results are never consumed: a valid predecessor is always
-        // an active wave's pixel (DESIGN.md "Slanted tiles").
-        const long long base = ((long long)(H - 1) * W + u) * D + e0;
+        // pixel of step s: row H-1-s (bottom-up) or s (top-down), column u+s.
+        // Steps where this wave's pixel lies outside the image load a clamped
+        // (valid) pixel, store to the dummy area, and their states are never
+        // consumed: a valid predecessor is always an active wave's pixel
+        // (DESIGN.md "Slanted tiles").
+        const long long base = ((long long)(UP ? H - 1 : 0) * W + u) * D + e0;
         const int s_lo = max(s_begin, -u), s_hi = min(s_end - 1, W - 1 - u);
         const bool never = s_lo > s_hi;
         auto off_of = [&](int s) -> long long {
             const int sc = uniform(min(max(s, s_lo), s_hi));
-            return never ? (long long)e0 : base - (long long)sc * dstep;
+            return never ? (long long)e0 : base + (long long)sc * dstep;
         };
-        float cb[PF][V], sb[PF][V], lb[PF][V], tb[PF][V];
+        constexpr int NS = UP ? 4 : 1;  // streams: C (+ S12, L3, T56)
+        float rb[NS][PF][V];
         int pfs = s_begin;  // step of the next ring refill
         auto refill = [&](int slot) {
             const long long o = off_of(pfs);
-            load_v<V>(cb[slot], sv.cost + o, dact);
+            load_v<V>(rb[0][slot], sv.cost + o, dact);
+            if constexpr (UP) {
 #ifndef SLANT_PROBE_NOLOADS
-            load_v_nt<V>(sb[slot], sv.s12 + o, dact);
-            load_v_nt<V>(lb[slot], sv.l3 + o, dact);
-            load_v_nt<V>(tb[slot], sv.t56 + o, dact);
+                load_v_nt<V>(rb[1][slot], sv.s12 + o, dact);
+                load_v_nt<V>(rb[2][slot], sv.l3 + o, dact);
+                load_v_nt<V>(rb[3][slot], sv.t56 + o, dact);
 #else
-            load_v<V>(sb[slot], sv.cost + o, dact);
-            load_v<V>(lb[slot], sv.cost + o, dact);
-            load_v<V>(tb[slot], sv.cost + o, dact);
+                load_v<V>(rb[1][slot], sv.cost + o, dact);
+                load_v<V>(rb[2][slot], sv.cost + o, dact);
+                load_v<V>(rb[3][slot], sv.cost + o, dact);
 #endif
+            }
             ++pfs;
         };
 #pragma unroll
         for (int q = 0; q < PF; ++q) refill(q);
-        float p7[V];
+        float po[V];  // the own (leaning) chain: L7 bottom-up, L5 top-down
 #pragma unroll
-        for (int v = 0; v < V; ++v) p7[v] = 0.0f;
-        float m7 = 0.0f;
+        for (int v = 0; v < V; ++v) po[v] = 0.0f;
+        float mo = 0.0f;
         lds_barrier();  // the courier's prologue phase
 #ifdef SGM_SLANT_STAMPS
         long long st_prev = __builtin_amdgcn_s_memtime(), st_work = 0, st_wait = 0;
@@ -312,60 +339,72 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
             const int j = u + s;
             const bool act = j >= 0 && j < W;
             const int pp = (s - 1) & 1, cp = s & 1;
-            // path starts (SGM.cpp:205-214, :321-335): a zero state before the
-            // first pixel makes the step yield L = C (P1, P2 >= 0)
-            const bool v4 = s >= 1, v7 = s >= 1 && j >= 1, v8 = s >= 1 && j + 1 <= W - 1;
-            float q4[V], q8[V], z7[V];
-            load_lds_v<V>(q4, &L.st[pp][k + 1][0][e0]);
-            load_lds_v<V>(q8, &L.st[pp][k + 2][1][e0]);
+            // path starts (SGM.cpp:93-98, :165-170, :205-214, :259-276,
+            // :321-335): a zero state before the first pixel makes the step
+            // yield L = C (P1, P2 >= 0)
+            const bool v1 = s >= 1, vo = s >= 1 && j >= 1, v2 = s >= 1 && j + 1 <= W - 1;
+            const float(&c)[V] = rb[0][q];
+            float q2[V], zo[V];
+            load_lds_v<V>(q2, &L.st[pp][k + 2][K2][e0]);
             // (uniform LDS words: into SGPRs, dp_step's scalar operand)
-            float m4 = uni_f(L.pm[pp][k + 1][0]), m8 = uni_f(L.pm[pp][k + 2][1]);
+            float m2 = uni_f(L.pm[pp][k + 2][K2]);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                q4[v] = v4 ? q4[v] : 0.0f;
-                q8[v] = v8 ? q8[v] : 0.0f;
-                z7[v] = v7 ? p7[v] : 0.0f;
+                q2[v] = v2 ? q2[v] : 0.0f;
+                zo[v] = vo ? po[v] : 0.0f;
             }
-            m4 = v4 ? m4 : 0.0f;
-            m8 = v8 ? m8 : 0.0f;
-            const float mm7 = v7 ? m7 : 0.0f;
-            float L4[V], L7[V], L8[V];
-            dp_step<V>(q4, m4, cb[q], L4, a.p1, p2v);
-            dp_step<V>(z7, mm7, cb[q], L7, a.p1, p2v);
-            dp_step<V>(q8, m8, cb[q], L8, a.p1, p2v);
-            const float n4 = wave_min(lane_min(L4)), n7 = wave_min(lane_min(L7)),
-                        n8 = wave_min(lane_min(L8));
-            float tot[V];
+            m2 = v2 ? m2 : 0.0f;
+            const float mmo = vo ? mo : 0.0f;
+            float Lo[V], L2[V];
+            dp_step<V>(zo, mmo, c, Lo, a.p1, p2v);
+            dp_step<V>(q2, m2, c, L2, a.p1, p2v);
+            const float no = wave_min(lane_min(Lo)), n2 = wave_min(lane_min(L2));
+            if constexpr (UP) {
+                float q1[V];
+                load_lds_v<V>(q1, &L.st[pp][k + 1][0][e0]);
+                float m1 = uni_f(L.pm[pp][k + 1][0]);
 #pragma unroll
-            for (int v = 0; v < V; ++v)
-                tot[v] = ((sb[q][v] + lb[q][v]) + L4[v]) + ((tb[q][v] + L7[v]) + L8[v]);
-            int d;
-            float f;
+                for (int v = 0; v < V; ++v) q1[v] = v1 ? q1[v] : 0.0f;
+                m1 = v1 ? m1 : 0.0f;
+                float L4[V];
+                dp_step<V>(q1, m1, c, L4, a.p1, p2v);
+                const float n4 = wave_min(lane_min(L4));
+                // ((S12 + L3) + L4) + ((T56 + L7) + L8)
+                float tot[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    tot[v] = ((rb[1][q][v] + rb[2][q][v]) + L4[v]) + ((rb[3][q][v] + Lo[v]) + L2[v]);
+                int d;
+                float f;
 #ifdef SLANT_PROBE_NOWTA
-            d = 0;  // timing probe: no WTA (wrong results)
-            f = tot[0];
+                d = 0;  // timing probe: no WTA (wrong results)
+                f = tot[0];
 #else
-            wta_subpixel<V>(tot, D, a.uniq, d, f);
+                wta_subpixel<V>(tot, D, a.uniq, d, f);
 #endif
-            store_lds_v<V>(&L.st[cp][k][0][e0], L4);
-            store_lds_v<V>(&L.st[cp][k][1][e0], L8);
-            if (lane == 0) {
-                L.pm[cp][k][0] = n4;
-                L.pm[cp][k][1] = n8;
-            }
-#pragma unroll
-            for (int v = 0; v < V; ++v) p7[v] = L7[v];
-            m7 = n7;
-            // outputs: an inactive step writes the dummy word instead
-            {
+                store_lds_v<V>(&L.st[cp][k][0][e0], L4);
+                if (lane == 0) L.pm[cp][k][0] = n4;
+                // outputs: an inactive step writes the dummy words instead
                 const long long pix = (long long)(H - 1 - s) * W + j;
-                float *fs = act ? sv.sub + pix : a.dummy;
+                float *fs = act ? sv.sub + pix : a.dummy + 256;
                 if (lane == 0) *fs = f;
                 if (sv.disp) {
-                    uint16_t *ds = act ? sv.disp + pix : reinterpret_cast<uint16_t *>(a.dummy + 1);
+                    uint16_t *ds = act ? sv.disp + pix : reinterpret_cast<uint16_t *>(a.dummy + 257);
                     if (lane == 0) *ds = (uint16_t)d;
                 }
+            } else {
+                // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
+                float o[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) o[v] = Lo[v] + L2[v];
+                float *dst = act ? sv.t56w + off_of(s) : a.dummy + e0;
+                store_v_nt<V>(dst, o, dact);
             }
+            store_lds_v<V>(&L.st[cp][k][K2][e0], L2);
+            if (lane == 0) L.pm[cp][k][K2] = n2;
+#pragma unroll
+            for (int v = 0; v < V; ++v) po[v] = Lo[v];
+            mo = no;
             refill(q);
 #ifdef SGM_SLANT_STAMPS
             const long long tb0 = __builtin_amdgcn_s_memtime();
@@ -402,11 +441,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_up_kernel(SlantArgs a, Ge
     // next launch's granule tag), so a replayed launch never reads this
     // launch's granules as its own
     if (tid_x() == 0) {
-        const unsigned n = atomicAdd(&a.ctl->exits, 1u);
+        const unsigned n = atomicAdd(&ctl->exits, 1u);
         if (n == (unsigned)a.grid - 1) {
-            atomicExch(&a.ctl->exits, 0u);
-            atomicExch(&a.ctl->tickets, 0u);
-            atomicAdd(&a.ctl->epoch, 1u);
+            atomicExch(&ctl->exits, 0u);
+            atomicExch(&ctl->tickets, 0u);
+            atomicAdd(&ctl->epoch, 1u);
         }
     }
 }
@@ -417,7 +456,8 @@ size_t slant_gran_count(Geom g, int nviews) {
     return (size_t)nviews * slant_tiles(g) * g.H * 3 * g.D;
 }
 
-hipError_t launch_slant_up(const SlantArgs &a0, Geom g, hipStream_t st) {
+template <bool UP>
+static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
     SlantArgs a = a0;
     a.ntiles = (int)slant_tiles(g);
     int dev = 0, cus = 0;
@@ -426,13 +466,27 @@ hipError_t launch_slant_up(const SlantArgs &a0, Geom g, hipStream_t st) {
         cus = 256;
     const int total = a.ntiles * a.nviews;
     a.grid = total < cus ? total : cus;
+#ifdef SGM_SLANT_DEBUG
+    if (const char *e = getenv("SGM_SLANT_GRID")) a.grid = atoi(e) > 0 && atoi(e) < a.grid ? atoi(e) : a.grid;
+#endif
     const dim3 grid(a.grid), block(64 * (kSlantNW + 1));
-    if (g.D == 32) slant_up_kernel<1, false, kSlantNW, 8, 3><<<grid, block, 0, st>>>(a, g);
-    else if (g.D == 64) slant_up_kernel<1, true, kSlantNW, 8, 3><<<grid, block, 0, st>>>(a, g);
-    else if (g.D == 128) slant_up_kernel<2, true, kSlantNW, 8, 3><<<grid, block, 0, st>>>(a, g);
-    else slant_up_kernel<4, true, kSlantNW, 4, 2><<<grid, block, 0, st>>>(a, g);
+    constexpr int PF4 = UP ? 4 : 8, PF = UP ? 8 : 16;
+    size_t pad = 0;
+#ifdef SGM_SLANT_DEBUG
+    if (const char *e = getenv("SGM_SLANT_LDSPAD")) pad = (size_t)atoi(e) * 1024;
+#endif
+    if (g.D == 32) slant_kernel<UP, 1, false, kSlantNW, PF, 3><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 3><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 3><<<grid, block, pad, st>>>(a, g);
+#ifndef SLANT_CR4
+#define SLANT_CR4 2
+#endif
+    else slant_kernel<UP, 4, true, kSlantNW, PF4, SLANT_CR4><<<grid, block, 0, st>>>(a, g);
     return hipGetLastError();
 }
+
+hipError_t launch_slant_up(const SlantArgs &a, Geom g, hipStream_t st) { return launch_slant_t<true>(a, g, st); }
+hipError_t launch_slant_down(const SlantArgs &a, Geom g, hipStream_t st) { return launch_slant_t<false>(a, g, st); }
 
 }  // namespace sgm
 

@@ -27,6 +27,23 @@ __global__ __launch_bounds__(64) void sweep_kernel(SweepArgs a, Geom g) {
     sweep_body<DIR, V, MODE, FULL, PF, BAND>(a, g, bid_x());
 }
 
+// The same sweep over both views' volumes (workgroup y = view): the L8 pass
+// of frames whose two cost volumes fit the Infinity Cache together (K64).
+template <int DIR, int V, int MODE, bool FULL, int PF>
+__global__ __launch_bounds__(64) void sweep2_kernel(SweepArgs a0, SweepArgs a1, Geom g) {
+    sweep_body<DIR, V, MODE, FULL, PF>(__builtin_amdgcn_workgroup_id_y() != 0 ? a1 : a0, g, bid_x());
+}
+
+hipError_t launch_sweep2_l8(const SweepArgs &a0, const SweepArgs &a1, Geom g, hipStream_t st) {
+    const dim3 grid(g.W, 2);
+    constexpr int PF = 16;
+    if (g.D == 32) sweep2_kernel<7, 1, SWEEP_ACC, false, PF><<<grid, 64, 0, st>>>(a0, a1, g);
+    else if (g.D == 64) sweep2_kernel<7, 1, SWEEP_ACC, true, PF><<<grid, 64, 0, st>>>(a0, a1, g);
+    else if (g.D == 128) sweep2_kernel<7, 2, SWEEP_ACC, true, PF><<<grid, 64, 0, st>>>(a0, a1, g);
+    else sweep2_kernel<7, 4, SWEEP_ACC, true, PF / 2><<<grid, 64, 0, st>>>(a0, a1, g);
+    return hipGetLastError();
+}
+
 // Diagonal INIT/ACC sweeps (the L8 pass): memory wave + DP wave
 // (sweep_split_body), blocks of 4 steps.
 template <int DIR, int V, int MODE, bool FULL>

@@ -29,8 +29,8 @@ torch.cuda.synchronize()
 prof = sgm.get_profile()
 lib.sgm_debug_slant_stamps(b, 1)
 x = list(b)
-print(f"{h}x{w} D={D} V={V}: slant_up {prof['slant_up'][1]:.3f} ms; workgroups {x[8]}, tiles {x[9]}, "
-      f"tile-steps {x[0]}")
+print(f"{h}x{w} D={D} V={V}: slant_up {prof['slant_up'][1]:.3f} ms, slant_down {prof['slant_down'][1]:.3f} ms "
+      f"(both passes below); workgroups {x[8]}, tiles {x[9]}, tile-steps {x[0]}")
 cyc = 100.0  # s_memtime ticks at 100 MHz on gfx950? (printed raw too)
 print("raw:", x[:10])
 steps = max(x[0], 1)
