@@ -82,6 +82,14 @@ def bytes_per_elem(name: str, D: int) -> float:
         # L6 fwd), then the whole H pair as its own launch
         "stage_a_d": 8.0 + (4.0 + ck),
         "stage_a_h": (4.0 + ck) + (8.0 + ck),
+        # the slanted-tile schedule (DESIGN.md "Slanted tiles"): vfwd writing
+        # the whole L3 volume; the top-down pass reads C and writes T56; the
+        # bottom-up pass reads C, S12, L3 and T56.  Each tile of NW = 14
+        # columns also hands 2 (top-down) or 3 (bottom-up) D-vectors per step
+        # to the next tile as 8-byte granules, written once and read once
+        "vfwd_l3": 12.0,
+        "slant_down": 8.0 + 2 * 16.0 / 14,
+        "slant_up": 16.0 + 3 * 16.0 / 14,
     }
     if name in table:
         return table[name]
@@ -98,7 +106,7 @@ def c_read_bytes_per_elem(name: str) -> float:
     table = {"stage_a": 12.0, "stage_b": 8.0, "pair_bwd_L4_final": 4.0, "sweep_L8_acc": 4.0,
              "stage_a_hp": 16.0, "stage_b_d2": 4.0, "stage_a_d": 8.0, "stage_a_h": 8.0,
              "pair_fwd_L1": 4.0, "pair_fwd_L3": 4.0, "pair_fwd_L6": 4.0,
-             "pair_bwd_L2_init2": 4.0, "pair_bwd_L7_acc": 4.0}
+             "pair_bwd_L2_init2": 4.0, "pair_bwd_L7_acc": 4.0, "slant_down": 4.0, "slant_up": 4.0}
     if name in table:
         return table[name]
     return 4.0 if name.startswith("sweep_") else 0.0

@@ -32,12 +32,9 @@ struct sgm_handle {
     Geom g;
     int device;
     int nviews;
-    int serialize;        // SGM_SERIALIZE=1: every kernel on one stream (isolated timings)
-    int concurrent_views; // SGM_CONCURRENT_VIEWS=1: right view on a second stream
     size_t bytes;
     hipStream_t st;       // the handle's own stream (host API, stages)
-    hipStream_t aux[1];      // right view (two-view frames)
-    hipEvent_t ev_ct, ev_c[2], ev_t[2], ev_s[2], ev_v1, ev_pf;
+    hipEvent_t ev_pf;     // the post filter's convergence readback
     hipEvent_t ev_last;   // the end of the last call's work on last_st (StreamScope)
     hipStream_t last_st;  // the stream of the last entry point's work (null: none yet)
     bool last_recorded;   // ev_last was recorded at the end of that call (a caller's stream)
@@ -61,12 +58,6 @@ struct sgm_handle {
     sgm::SlantCtl *d_slant_ctl;  // slant: launch bookkeeping of the passes
     float *d_slant_dummy;        // slant: the target of inactive lanes' stores
     int band_rows;        // rows per band of the backward phase (0: whole volume)
-    bool fwd_bands;       // frames also run vfwd and stage A's diagonal roles in bands
-    bool sub_cm;          // two-view frames: column-major sub-pixel maps + lr_cm_kernel
-                          // (SGM_SUB_CM=0: row-major maps + lr_kernel)
-    bool t56;             // SGM_T56=1 (banded frames): T56 = L5 + L6 in the forward bands,
-                          // L7 as a plain sweep in the backward bands (DESIGN.md lever 2)
-    int fwd_band_rows;    // rows per forward band (a multiple of 16)
     int mf_rows;          // median fill tile rows (4 or 8 by frame size; SGM_MF_ROWS)
     // post_filter scratch (sgm_post.hip)
     float *d_pf_orig;     // the map as it entered the median fill
@@ -247,9 +238,7 @@ void free_all(sgm_handle *h) {
     for (auto &v : h->d_ck)
         for (auto p : v) (void)hipFree(p);
     if (h->st) (void)hipStreamDestroy(h->st);
-    for (auto &s : h->aux) if (s) (void)hipStreamDestroy(s);
-    hipEvent_t evs[] = {h->ev_ct, h->ev_c[0], h->ev_c[1], h->ev_t[0], h->ev_t[1],
-                        h->ev_s[0], h->ev_s[1], h->ev_v1, h->ev_pf, h->ev_last};
+    hipEvent_t evs[] = {h->ev_pf, h->ev_last};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -371,11 +360,13 @@ int band_rows_for(Geom g) {
 //   final:   L4 bwd recomputing L3: total = ((S12 + L3) + L4) + T -> WTA
 // (the reference's order, SGM.cpp:386-390).  T may alias the dead
 // horizontally filtered volume.
-// fwd_bands (banded frames): the view's vertical filter + L3 forward pass
-// (vfwd, from the horizontally filtered volume T) and stage A's diagonal
-// roles run in forward bands first, top band first, so that each band's
-// final cost stays in the Infinity Cache from vfwd to L5 and L6; the whole H
-// pair follows as its own launch (DESIGN.md "Bands").
+// Banded frames (cost volumes above the Infinity Cache): the view's vertical
+// filter + L3 forward pass (vfwd, from the horizontally filtered volume T)
+// and stage A's diagonal roles run in forward bands first, top band first, so
+// that each band's final cost stays in the Infinity Cache from vfwd to L5 and
+// L6; the whole H pair follows as its own launch; then the backward bands
+// (DESIGN.md "Bands").  need_v_ckpt (the parity stage, from a final cost
+// volume) runs whole-volume passes.
 // part AGG_FWD stops after the forward bands and leaves the H pair's
 // arguments in hp[0..1] (the caller launches both views' H pairs at once);
 // AGG_BWD then runs the rest.
@@ -387,8 +378,7 @@ inline float *cost_buf(sgm_handle *h, int v) { return h->d_c[v]; }
 inline float *t_buf(sgm_handle *h, int v) { return h->d_ch[v]; }
 int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *T, uint16_t *disp,
                    float *sub, hipStream_t st, bool need_v_ckpt, sgm::PairArgs *defer_final = nullptr,
-                   bool fwd_bands = false, int part = AGG_ALL, sgm::PairArgs *hp = nullptr,
-                   int sub_cm = 0) {
+                   int part = AGG_ALL, sgm::PairArgs *hp = nullptr, int sub_cm = 0) {
     float **ck = h->d_ck[view];
     const double elems = (double)h->g.H * h->g.W * h->g.D;
     sgm::PairArgs pa = pair_args(h);
@@ -407,18 +397,17 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     h2.out = S;
     d7.acc_in = T;
     d7.out = T;
-    const int H = h->g.H, BR = h->band_rows;
-    // banded: stage A runs the whole H pair (S12), stage B's bands only the
-    // diagonal pair
-    const bool banded = BR > 0 && !defer_final;
+    const int H = h->g.H;
+    const bool banded = h->band_rows > 0 && !defer_final && !need_v_ckpt;
+    const int BR = banded ? h->band_rows : 0;
     if (part == AGG_BWD) {
         // stage A ran (AGG_FWD + the caller's H pair launch)
-    } else if (banded && fwd_bands) {
+    } else if (banded) {
         sgm::PairArgs va = pair_args(h);
         va.ckpt = ck[sgm::PAIR_V];
         // band edges at H - m*BR (multiples of 16 rows from the bottom, as
         // the backward bands): whole segments of every family
-        const int FR = h->fwd_band_rows;
+        const int FR = BR;
         const int nb = (H + FR - 1) / FR;
         for (int m = nb - 1; m >= 0; --m) {
             const int rb = H - (m + 1) * FR > 0 ? H - (m + 1) * FR : 0, re = H - m * FR;
@@ -429,22 +418,8 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
                    }));
             l5.band = {rb, re, h->d_carry[view][0]};
             d6.band = {rb, re, h->d_carry[view][1]};
-            if (h->t56) {
-                // T56 = L5 + L6 (SGM.cpp:389's first association): L5 writes T
-                // and the L6 sweep adds into it while the band is cached
-                HIPCHK(h, timed(h, "sweep_L5_init", be, st, [&] {
-                           return sgm::launch_sweep(SGM_DIR_L5, sgm::SWEEP_INIT, l5, h->g, st);
-                       }));
-                SweepArgs l6 = l5;
-                l6.acc_in = T;
-                l6.band = d6.band;
-                HIPCHK(h, timed(h, "sweep_L6_acc", be, st, [&] {
-                           return sgm::launch_sweep(SGM_DIR_L6, sgm::SWEEP_ACC, l6, h->g, st);
-                       }));
-            } else {
-                HIPCHK(h, timed(h, "stage_a_d", be, st,
-                                [&] { return sgm::launch_stage_a_band(l5, d6, h->g, st); }));
-            }
+            HIPCHK(h, timed(h, "stage_a_d", be, st,
+                            [&] { return sgm::launch_stage_a_band(l5, d6, h->g, st); }));
         }
         if (part == AGG_FWD) {
             hp[0] = h1;
@@ -454,11 +429,10 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
         HIPCHK(h, timed(h, "stage_a_h", elems, st,
                         [&] { return sgm::launch_stage_a_hpair(&h1, &h2, 1, h->g, st); }));
     } else {
-        HIPCHK(h, timed(h, banded ? "stage_a_hp" : "stage_a", elems, st, [&] {
-                   return sgm::launch_stage_a(h1, l5, d6, h->g, st, banded ? &h2 : nullptr);
-               }));
+        HIPCHK(h, timed(h, "stage_a", elems, st,
+                        [&] { return sgm::launch_stage_a(h1, l5, d6, h->g, st); }));
     }
-    if (BR == 0 || defer_final)
+    if (!banded)
         HIPCHK(h, timed(h, "stage_b", elems, st,
                         [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
     SweepArgs l8 = sweep_args(h);
@@ -471,25 +445,14 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     pa.disp = disp;
     pa.sub = sub;
     pa.sub_cm = sub_cm;
-    if (BR > 0 && !defer_final) {
+    if (banded) {
         // bottom band first: the backward passes walk up
         for (int kb = 0; kb < H; kb += BR) {
             const int ke = kb + BR < H ? kb + BR : H;
             const double be = (double)(ke - kb) / H * elems;
             d7.band = {kb, ke, h->d_carry[view][0]};
-            if (h->t56) {  // T = T56 + L7: a plain sweep, no L6 recompute
-                SweepArgs l7 = sweep_args(h);
-                l7.cost = cost;
-                l7.acc_in = T;
-                l7.acc_out = T;
-                l7.band = d7.band;
-                HIPCHK(h, timed(h, "sweep_L7_acc", be, st, [&] {
-                           return sgm::launch_sweep(SGM_DIR_L7, sgm::SWEEP_ACC, l7, h->g, st);
-                       }));
-            } else {
-                HIPCHK(h, timed(h, "stage_b_d2", be, st,
-                                [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
-            }
+            HIPCHK(h, timed(h, "stage_b_d2", be, st,
+                            [&] { return sgm::launch_stage_b(h2, d7, h->g, st); }));
             l8.band = {kb, ke, h->d_carry[view][1]};
             pa.band = {kb, ke, h->d_carry[view][2]};
             HIPCHK(h, timed(h, "sweep_L8_acc", be, st,
@@ -653,6 +616,19 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     sa.p2 = (float)h->p.p2;
     sa.uniq = h->p.uniqueness;
     sa.nviews = nv;
+#ifdef SGM_SLANT_DEBUG
+    if (getenv("SGM_SLANT_T56SWEEP")) {  // T56 by the two diagonal sweeps instead
+        for (int v = 0; v < nv; ++v) {
+            SweepArgs l5 = sweep_args(h);
+            l5.cost = h->d_c[v];
+            l5.acc_out = t_buf(h, v);
+            HIPCHK(h, sgm::launch_sweep(SGM_DIR_L5, sgm::SWEEP_INIT, l5, g, st));
+            SweepArgs l6 = l5;
+            l6.acc_in = t_buf(h, v);
+            HIPCHK(h, sgm::launch_sweep(SGM_DIR_L6, sgm::SWEEP_ACC, l6, g, st));
+        }
+    } else
+#endif
     HIPCHK(h, timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); }));
     HIPCHK(h, timed(h, "stage_a_h", nv * elems, st,
                     [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, st); }));
@@ -665,15 +641,16 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
               int out_pitch, uint16_t *d_raw, hipStream_t st) {
     const Geom g = h->g;
     int rc;
-    // Views run back to back on one stream by default: each view's cost
-    // volume (238.5 MB at K128) then stays resident in the 256 MB Infinity
-    // Cache through its six readers, which concurrent views would thrash
-    // (1.589 vs 1.627 ms per K128 pair).  SGM_CONCURRENT_VIEWS=1 restores the
-    // second stream.
+    // Everything runs on one stream.  Two-view frames keep each view's cost
+    // volume resident in the 256 MB Infinity Cache through its readers by
+    // running the views' aggregation back to back (K128: 238.5 MB per view;
+    // concurrent views measured 1.627 vs 1.589 ms per pair), unless both
+    // volumes fit together (K64: joint launches) or neither fits (HD/4K:
+    // bands, or the slanted schedule).
     if (h->p.solver == SGM_SOLVER_BM)
         return bm_frame(h, d_left, d_right, pitch, d_sky_l, sky_pitch, d_out, out_pitch, d_raw, st);
-    hipStream_t aux1 = h->concurrent_views ? h->aux[0] : st;  // right view
     const double npx = (double)g.H * g.W;
+    const double vol_bytes = npx * g.D * sizeof(float);
     // a right-view handle (SGM_VIEW_RIGHT) runs the right view in slot 0
     const bool right_only = h->p.view == SGM_VIEW_RIGHT;
     if (h->p.sky_detect) {  // node.cpp:80-93: detect on both inputs, then process with the masks
@@ -690,102 +667,80 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                return sgm::launch_census(d_left, pitch, g, h->p.blur, h->d_ct[0], st, false,
                                          d_right, h->d_ct[1]);
            }));
-    // Events only where a second stream joins: on ROCm every event record in
-    // a stream costs the next kernel ~6 us of dispatch gap (measured, rocprof
-    // kernel trace), three of them per K128 frame before this was restricted.
-    // two views on one stream: both DSIs + horizontal IIRs in one launch (a
-    // view's H*D serial chains alone leave most SIMDs idle at KITTI sizes)
-    const bool both_h = h->nviews == 2 && aux1 == st && (d_sky_l == nullptr) == (d_sky_r == nullptr) &&
+    // two views: both DSIs + horizontal IIRs in one launch (a view's H*D
+    // serial chains alone leave most SIMDs idle at KITTI sizes)
+    const bool both_h = h->nviews == 2 && (d_sky_l == nullptr) == (d_sky_r == nullptr) &&
                         sgm::cost_h2_supported(g, d_sky_l != nullptr);
-    if (h->nviews == 2 && !both_h && aux1 != st) HIPCHK(h, hipEventRecord(h->ev_ct, st));
     // banded frames run vfwd in forward bands inside aggregate_view; the
     // slanted schedule runs its own vertical pass
-    const bool fwd_bands = h->fwd_bands || h->slant;
+    const bool banded = h->band_rows > 0;
+    const bool vfwd_here = !banded && !h->slant;
     if (both_h) {
         HIPCHK(h, timed(h, "cost_h", 2.0 * npx * g.D, st, [&] {
                    return sgm::launch_cost_h2(h->d_ct[0], h->d_ct[1], d_sky_l, d_sky_r, sky_pitch, g,
                                               h->d_ch[0], h->d_ch[1], st);
                }));
-        if (!fwd_bands) {
+        if (vfwd_here) {
             if ((rc = vfwd_view(h, 1, st)) != SGM_OK) return rc;
             if ((rc = vfwd_view(h, 0, st)) != SGM_OK) return rc;
         }
     } else {
-        if (h->nviews == 2) {
-            if (aux1 != st) HIPCHK(h, hipStreamWaitEvent(aux1, h->ev_ct, 0));
-            if ((rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, aux1, !fwd_bands)) != SGM_OK) return rc;
-        }
+        if (h->nviews == 2 && (rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, st, vfwd_here)) != SGM_OK)
+            return rc;
         if ((rc = cost_view(h, 0, right_only ? 1 : 0, right_only ? d_sky_r : d_sky_l, sky_pitch,
-                            st, !fwd_bands)) != SGM_OK)
+                            st, vfwd_here)) != SGM_OK)
             return rc;
     }
-    // Volumes larger than the 256 MB Infinity Cache gain nothing from
-    // finishing the left view first: both views' final passes then run as one
-    // launch (fewer workgroup rounds at HD/4K)
-    const bool both_final = h->nviews == 2 && aux1 == st && h->band_rows == 0 &&
-                            (double)g.H * g.W * g.D * sizeof(float) > 256.0 * 1024 * 1024 &&
-                            !getenv("SGM_SPLIT_FINAL");
-    sgm::PairArgs fin[2];
     // one view with a dense output map: the final pass writes the sub-pixel
     // map straight into it (no device copy after the frame)
     const bool direct_out = h->nviews == 1 && out_pitch == g.W;
     float *sub0 = direct_out ? d_out : h->d_sub[0];
+    // two views: the final passes write column-major sub-pixel maps (whole
+    // cache lines; lr_cm_kernel reads them through LDS tiles); the slanted
+    // pass writes row-major ones
+    const bool cm = h->nviews == 2 && !h->slant;
     if (h->slant) {
         if ((rc = slant_views(h, sub0, d_raw, st)) != SGM_OK) return rc;
-        if (h->nviews == 2) {
-            HIPCHK(h, timed(h, "lr", npx, st, [&] {
-                       return sgm::launch_lr(h->d_sub[0], g.W, h->d_sub[1], g.W, d_out, out_pitch,
-                                             h->p.lr_max_diff, g, st);
-                   }));
-        } else if (!direct_out) {
-            HIPCHK(h, hipMemcpy2DAsync(d_out, (size_t)out_pitch * sizeof(float), h->d_sub[0],
-                                       (size_t)g.W * sizeof(float), (size_t)g.W * sizeof(float), g.H,
-                                       hipMemcpyDeviceToDevice, st));
-        }
-        return finish_frame(h, d_left, d_right, pitch, d_out, out_pitch, st);
-    }
-    // two views whose cost volumes fit the Infinity Cache together: joint
-    // launches (aggregate_joint)
-    const bool joint = h->nviews == 2 && aux1 == st && h->band_rows == 0 &&
-                       2.0 * g.H * g.W * g.D * sizeof(float) <= 256.0 * 1024 * 1024;
-    // banded frames with two views on one stream: both views' forward bands,
-    // then both H pairs in one launch, then each view's backward bands
-    const bool split_h = fwd_bands && h->nviews == 2 && aux1 == st;
-    if (split_h) {
+    } else if (h->nviews == 2 && !banded && 2.0 * vol_bytes <= 256.0 * 1024 * 1024) {
+        // both volumes fit the Infinity Cache together: joint launches
+        if ((rc = aggregate_joint(h, sub0, d_raw, 1, st)) != SGM_OK) return rc;
+    } else if (h->nviews == 2 && banded) {
+        // both views' forward bands, then both H pairs in one launch, then
+        // each view's backward bands
         sgm::PairArgs hp[2][2];
         for (int v = 0; v < 2; ++v)
             if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), v ? nullptr : d_raw,
-                                     v ? h->d_sub[1] : sub0, st, false, nullptr, true, AGG_FWD,
+                                     v ? h->d_sub[1] : sub0, st, false, nullptr, AGG_FWD,
                                      hp[v])) != SGM_OK)
                 return rc;
         const sgm::PairArgs h1[2] = {hp[0][0], hp[1][0]}, h2[2] = {hp[0][1], hp[1][1]};
         HIPCHK(h, timed(h, "stage_a_h", 2.0 * npx * g.D, st,
                         [&] { return sgm::launch_stage_a_hpair(h1, h2, 2, g, st); }));
-    }
-    const int part = split_h ? AGG_BWD : AGG_ALL;
-    // two views: the final passes write column-major sub-pixel maps (whole
-    // cache lines; lr_cm_kernel reads them through LDS tiles)
-    const int cm = h->nviews == 2 && h->sub_cm ? 1 : 0;
-    if (joint) {
-        if ((rc = aggregate_joint(h, sub0, d_raw, cm, st)) != SGM_OK) return rc;
-    } else if ((rc = aggregate_view(h, 0, cost_buf(h, 0), h->d_s[0], t_buf(h, 0), d_raw, sub0, st,
-                                    false, both_final ? &fin[0] : nullptr, fwd_bands, part, nullptr,
-                                    cm)) != SGM_OK) {
-        return rc;
+        for (int v = 0; v < 2; ++v)
+            if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), v ? nullptr : d_raw,
+                                     v ? h->d_sub[1] : sub0, st, false, nullptr, AGG_BWD, nullptr,
+                                     1)) != SGM_OK)
+                return rc;
+    } else if (h->nviews == 2 && vol_bytes > 256.0 * 1024 * 1024) {
+        // whole-volume passes above the Infinity Cache (SGM_BAND_ROWS=0):
+        // nothing is gained by finishing the left view first, so both
+        // views' final passes run as one launch (fewer workgroup rounds)
+        sgm::PairArgs fin[2];
+        for (int v = 0; v < 2; ++v)
+            if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), v ? nullptr : d_raw,
+                                     v ? h->d_sub[1] : sub0, st, false, &fin[v], AGG_ALL, nullptr,
+                                     1)) != SGM_OK)
+                return rc;
+        HIPCHK(h, timed(h, "pair_bwd_L4_final", 2.0 * npx * g.D, st,
+                        [&] { return sgm::launch_final2(fin[0], fin[1], g, st); }));
+    } else {
+        for (int v = 0; v < h->nviews; ++v)
+            if ((rc = aggregate_view(h, v, cost_buf(h, v), h->d_s[v], t_buf(h, v), v ? nullptr : d_raw,
+                                     v ? h->d_sub[1] : sub0, st, false, nullptr, AGG_ALL, nullptr,
+                                     cm ? 1 : 0)) != SGM_OK)
+                return rc;
     }
     if (h->nviews == 2) {
-        if (!joint &&
-            (rc = aggregate_view(h, 1, cost_buf(h, 1), h->d_s[1], t_buf(h, 1), nullptr, h->d_sub[1],
-                                 aux1, false, both_final ? &fin[1] : nullptr, fwd_bands,
-                                 part, nullptr, cm)) != SGM_OK)
-            return rc;
-        if (both_final)
-            HIPCHK(h, timed(h, "pair_bwd_L4_final", 2.0 * npx * g.D, st,
-                            [&] { return sgm::launch_final2(fin[0], fin[1], g, st); }));
-        if (aux1 != st) {
-            HIPCHK(h, hipEventRecord(h->ev_v1, aux1));
-            HIPCHK(h, hipStreamWaitEvent(st, h->ev_v1, 0));
-        }
         HIPCHK(h, timed(h, "lr", npx, st, [&] {
                    return cm ? sgm::launch_lr_cm(h->d_sub[0], h->d_sub[1], d_out, out_pitch,
                                                  h->p.lr_max_diff, g, st)
@@ -976,13 +931,6 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
     h->g.W = p->width / p->scale;
     h->g.D = p->max_disp;
     h->nviews = p->views;
-    {
-        const char *ser = getenv("SGM_SERIALIZE");
-        h->serialize = ser && ser[0] == '1';
-        const char *cv = getenv("SGM_CONCURRENT_VIEWS");
-        h->concurrent_views = cv && cv[0] == '1' && !h->serialize;
-    }
-
     const size_t npx = (size_t)h->g.H * h->g.W;
     const size_t nvol = npx * h->g.D;
     const size_t nin = (size_t)p->height * p->width;
@@ -990,12 +938,7 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
     int rc = SGM_OK;
     do {
         if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
-        for (auto &s : h->aux)
-            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { rc = SGM_ERR_HIP; break; }
-        if (rc) break;
-        hipEvent_t *evs[] = {&h->ev_ct, &h->ev_c[0], &h->ev_c[1], &h->ev_t[0], &h->ev_t[1],
-                             &h->ev_s[0], &h->ev_s[1], &h->ev_v1, &h->ev_pf,
-                             &h->ev_last};
+        hipEvent_t *evs[] = {&h->ev_pf, &h->ev_last};
         for (auto e : evs) {
             // stream-to-stream ordering on this device needs no system-scope
             // fence (L2 writeback/invalidate); the post filter's host
@@ -1045,18 +988,6 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
                 rc = set_err(h, SGM_ERR_HIP, "hipMemset of the slanted schedule's hand-off state failed");
         }
         h->band_rows = band_rows_for(h->g);
-        {
-            const char *e = getenv("SGM_FWD_BANDS");
-            h->fwd_bands = h->band_rows > 0 && !(e && *e == '0');
-            // forward bands may differ in size (SGM_FWD_BAND_ROWS, multiples of 16)
-            const char *f = getenv("SGM_FWD_BAND_ROWS");
-            const int fr = f && *f ? atoi(f) / 16 * 16 : 0;
-            h->fwd_band_rows = fr > 0 ? fr : h->band_rows;
-            const char *cmv = getenv("SGM_SUB_CM");
-            h->sub_cm = !(cmv && *cmv == '0');
-            const char *t = getenv("SGM_T56");
-            h->t56 = h->fwd_bands && t && *t == '1';
-        }
         if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
             for (int v = 0; v < 2 && !rc; ++v) {
                 if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
@@ -1292,7 +1223,6 @@ int sgm_stage_aggregate(sgm_handle *h, const float *cost, uint16_t *disp, float 
     StreamScope scope(h, nullptr);
     const size_t npx = (size_t)h->g.H * h->g.W, nvol = npx * h->g.D;
     HIPCHK(h, hipMemcpyAsync(h->d_c[0], cost, nvol * 4, hipMemcpyHostToDevice, h->st));
-    HIPCHK(h, hipEventRecord(h->ev_c[0], h->st));
     int rc = aggregate_view(h, 0, h->d_c[0], h->d_s[0], h->d_ch[0], h->d_disp[0], h->d_sub[0],
                             h->st, true);
     if (rc) return rc;

@@ -108,11 +108,11 @@ hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStre
 // cost_vertical_filter (Solver.cpp:333-368) fused with the L3 forward pass:
 // in = horizontally filtered volume, out = final cost volume, a.ckpt = L3
 // checkpoints.
-// Multi-role launches of the frame schedule (sgm_pair.hip).
-// h2 (the banded schedule): stage A also runs the H pair's backward half
-// into h2.out, and banded stage B launches (d7.band) run no H rows
+// Multi-role launches of the frame schedule (sgm_pair.hip); banded stage B
+// launches (d7.band) run no H rows (the banded schedule's H pair is its own
+// launch)
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
-                          hipStream_t st, const PairArgs *h2 = nullptr);
+                          hipStream_t st);
 hipError_t launch_stage_b(const PairArgs &h2, const PairArgs &d7, Geom g, hipStream_t st);
 // both views' stage A / stage B / L8 sweep in one launch each (grid.y = view;
 // arrays of two)
@@ -133,8 +133,9 @@ hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs
                           hipStream_t st);
 
 // ----------------------------------------------- slanted tiles (sgm_slant.hip)
-// Compute waves per tile (one more wave per workgroup carries the hand-offs).
-constexpr int kSlantNW = 15;
+// Compute waves per tile (two more waves per workgroup carry the hand-offs:
+// one publishes the tile's exit states, one receives the next tile's).
+constexpr int kSlantNW = 14;
 // Launch bookkeeping of one slanted pass kind, in device memory (zeroed at
 // create): tickets claim tiles, the last workgroup out resets tickets/exits
 // and advances epoch (the hand-off granules' tag), err counts hang-guard

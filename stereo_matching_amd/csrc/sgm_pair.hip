@@ -87,19 +87,13 @@ __global__ __launch_bounds__(256) void pair_final2_kernel(PairArgs a0, PairArgs 
 // H blocks come first so they start at once.
 //   stage A: L1 forward (ckpt)  |  L5 -> T5         |  L6 forward (ckpt)
 //   stage B: L2 backward -> S12 |  L7 backward: T = (T5 + L6) + L7
-// HP (the banded schedule, volumes above the Infinity Cache): an H block
-// also runs its row's backward half (L2 recomputing L1 from the checkpoints
-// it has just written -> S12), so that the banded stage B launches carry no
-// whole-row chains.  (Two-wave blocks running the backward half split over
-// both waves, as stage B does, were slower: the split's LDS ring on every
-// block of the launch cuts the diagonal roles' occupancy.)
-// ROLES 1 (the forward bands): the diagonal roles only, steps [kb, ke) of each
-// chain (l5.band, d6.band); the H pair then runs as its own launch (grid H,
-// HP) after the last forward band -- its whole-row chains would set every
-// band launch's length.
-template <int V, bool FULL, bool HP, int ROLES = 0>
+// ROLES 1 (the forward bands, volumes above the Infinity Cache): the
+// diagonal roles only, steps [kb, ke) of each chain (l5.band, d6.band); the
+// H pair then runs as its own launch (hpair_kernel) after the last forward
+// band -- its whole-row chains would set every band launch's length.
+template <int V, bool FULL, int ROLES = 0>
 __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, PairArgs d6,
-                                                     PairArgs h2, Geom g) {
+                                                     Geom g) {
     constexpr int PFH = V >= 4 ? 16 : 32, PFD = V >= 4 ? 8 : 16;
     int b = bid_x();
     if constexpr (ROLES == 1) {
@@ -111,10 +105,6 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
         // the H chains (few, long) are the launch's critical path
         __builtin_amdgcn_s_setprio(3);
         pair_fwd_body<0, V, FULL, PFH>(h1, g, b);
-        if constexpr (HP) {
-            __threadfence();  // this wave's checkpoint stores, before it reads them back
-            pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, b, nullptr, nullptr);
-        }
         return;
     }
     b -= g.H;
@@ -125,8 +115,8 @@ __global__ __launch_bounds__(64) void stage_a_kernel(PairArgs h1, SweepArgs l5, 
     pair_fwd_body<5, V, FULL, PFD>(d6, g, b - g.W);
 }
 
-// The forward bands' H pair (L1 forward, then L2 backward recomputing L1 ->
-// S12, as stage_a_kernel<.., HP>'s H blocks) of one or two views in one
+// The forward bands' H pair (L1 forward, then L2 backward recomputing L1 from
+// the checkpoints it has just written -> S12) of one or two views in one
 // launch (workgroup y = view).  With the diagonal roles in the band launches
 // this launch holds only H (per view) single-wave chains, about one per SIMD
 // at HD256, so it waits on memory latency; both views' rows side by side
@@ -151,8 +141,8 @@ __global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, P
 // recompute wave and a backward wave (pair_split_body); a D2 block runs two
 // anti-diagonal L7 chains, one per wave.
 // HROWS = false: a banded stage B (d7.band: the diagonal pair's steps
-// [kb, ke)) without H rows -- the banded schedule's stage A ran them
-// (stage_a_kernel<.., HP>).
+// [kb, ke)) without H rows -- the banded schedule's H pair ran them
+// (hpair_kernel).
 template <int V, bool FULL, bool HROWS>
 __global__ __launch_bounds__(128) void stage_b_kernel(PairArgs h2, PairArgs d7, Geom g) {
     constexpr int K = pair_k<V>();
@@ -224,20 +214,19 @@ hipError_t launch_stage_b2(const PairArgs *h2, const PairArgs *d7, Geom g, hipSt
     return hipGetLastError();
 }
 
-template <bool HP, int ROLES = 0>
-static void launch_stage_a_t(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6,
-                             const PairArgs &h2, Geom g, hipStream_t st, int nblk) {
+template <int ROLES = 0>
+static void launch_stage_a_t(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
+                             hipStream_t st, int nblk) {
     const dim3 grid(nblk);
-    if (g.D == 32) stage_a_kernel<1, false, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
-    else if (g.D == 64) stage_a_kernel<1, true, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
-    else if (g.D == 128) stage_a_kernel<2, true, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
-    else stage_a_kernel<4, true, HP, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, h2, g);
+    if (g.D == 32) stage_a_kernel<1, false, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    else if (g.D == 64) stage_a_kernel<1, true, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    else if (g.D == 128) stage_a_kernel<2, true, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, g);
+    else stage_a_kernel<4, true, ROLES><<<grid, 64, 0, st>>>(h1, l5, d6, g);
 }
 
 hipError_t launch_stage_a(const PairArgs &h1, const SweepArgs &l5, const PairArgs &d6, Geom g,
-                          hipStream_t st, const PairArgs *h2) {
-    if (h2) launch_stage_a_t<true>(h1, l5, d6, *h2, g, st, g.H + 2 * g.W);
-    else launch_stage_a_t<false>(h1, l5, d6, h1, g, st, g.H + 2 * g.W);
+                          hipStream_t st) {
+    launch_stage_a_t(h1, l5, d6, g, st, g.H + 2 * g.W);
     return hipGetLastError();
 }
 
@@ -253,7 +242,7 @@ hipError_t launch_stage_a_hpair(const PairArgs *h1, const PairArgs *h2, int nvie
 }
 
 hipError_t launch_stage_a_band(const SweepArgs &l5, const PairArgs &d6, Geom g, hipStream_t st) {
-    launch_stage_a_t<false, 1>(d6, l5, d6, d6, g, st, 2 * g.W);
+    launch_stage_a_t<1>(d6, l5, d6, g, st, 2 * g.W);
     return hipGetLastError();
 }
 

@@ -118,7 +118,7 @@ struct SlantExits {
 // rings stay in flight across steps (a branch around a memory instruction
 // makes later waits drain everything outstanding).
 template <bool UP, int V, bool FULL, int NW, int PF, int CR>
-__global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom g) {
+__global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom g) {
     constexpr int NE = UP ? 2 : 1;         // states exchanged per wave
     constexpr int K2 = UP ? 1 : 0;         // index of the wave k+2 family (L8 / L6)
     using X = SlantExits<UP>;
@@ -128,6 +128,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
     const int H = g.H, W = g.W, D = g.D;
     const int e0 = lane * V;
     const bool dact = FULL || e0 < D;
+    // granule offset of this lane: lanes past D (D = 32) read lane 0's and
+    // store nothing (their e0 would run into the next slot)
+    const int eg = dact ? e0 : 0;
     const int T = a.ntiles, total = T * a.nviews;
     SlantCtl *ctl = a.ctl + (UP ? 1 : 0);
     // one step: up-right (-W*D + D) bottom-up, down-right (W*D + D) top-down
@@ -154,17 +157,41 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         const int s_end = min(H, W - u_lo);
         const int nsteps = s_end - s_begin;
 
+        if (wave == NW + 1) {
+            // ---------------------------------------------- publisher wave
+            // Phase p (p = 0 .. nsteps, each ending on the tile's barrier)
+            // publishes this tile's exit states of step s_begin + p - 2,
+            // which waves 0 and 1 wrote to LDS in the step that ended at the
+            // previous barrier (the compute waves run step s_begin + p - 1
+            // meanwhile); the last step goes out after the last barrier.
+            // Stores only: its waits never hold the receiver's loads.
+            auto publish = [&](int sp) {
+                const int par = sp & 1;
+                unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t, sp, 0) + eg;
+#pragma unroll
+                for (int x = 0; x < NX; ++x) {
+                    float y[V];
+                    load_lds_v<V>(y, &L.st[par][X::wave(x)][X::kind(x)][e0]);
+                    if (dact) store_granules<V>(gb + x * D, y, tag);
+                }
+            };
+            lds_barrier();
+            if (nsteps >= 1) lds_barrier();
+            for (int p = 2; p <= nsteps; ++p) {
+                publish(s_begin + p - 2);
+                lds_barrier();
+            }
+            publish(s_end - 1);
+            continue;
+        }
         if (wave == NW) {
-            // ------------------------------------------------ courier wave
+            // ----------------------------------------------- receiver wave
             // Phase p = 0 .. nsteps (the prologue, then one per step; each
-            // ends on the tile's barrier):
-            //  * publishes this tile's exit states of step s_begin + p - 1
-            //    (its waves 0 and 1 wrote them to LDS in that step) as
-            //    granules;
-            //  * hands the next tile's exit states of step gs = s_begin - 1 + p
-            //    to LDS parity gs & 1 (slots NW, NW+1), which step gs + 1
-            //    reads.  Their granule loads run CR phases ahead; a phase
-            //    re-polls only when the next tile is not that far ahead.
+            // ends on the tile's barrier) hands the next tile's exit states
+            // of step gs = s_begin - 1 + p to LDS parity gs & 1 (slots NW,
+            // NW+1), which step gs + 1 reads.  Their granule loads run CR
+            // phases ahead; a phase re-polls only when the next tile is not
+            // that far ahead.
             auto gvalid = [&](int p) {
                 return t + 1 < T && (p >= 1 || s_begin >= 1) && p < nsteps;
             };
@@ -175,7 +202,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 const bool ok = gvalid(p);
                 const int tt = uniform(ok ? t + 1 : t);
                 const int ss = uniform(ok ? s_begin - 1 + p : s_begin);
-                return sv.gran + gran_index(T, H, D, view, tt, ss, 0) + e0;
+                return sv.gran + gran_index(T, H, D, view, tt, ss, 0) + eg;
             };
             unsigned long long rq[CR][NX][V];
             auto issue = [&](int slot, int p) {
@@ -190,24 +217,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                         rq[slot][x][v] = __hip_atomic_load(const_cast<unsigned long long *>(gb + x * D + v),
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             };
-            auto publish = [&](int sp) {
-                const int par = sp & 1;
-                unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t, sp, 0) + e0;
-#pragma unroll
-                for (int x = 0; x < NX; ++x) {
-                    float y[V];
-                    load_lds_v<V>(y, &L.st[par][X::wave(x)][X::kind(x)][e0]);
-                    store_granules<V>(gb + x * D, y, tag);
-                }
-            };
 #pragma unroll
             for (int q = 0; q < CR; ++q) issue(q, q);
             auto phase = [&](int slot, int p) {
-                // 1) publish this tile's step s_begin + p - 2, completed at the
-                // barrier that ended the previous phase (the compute waves run
-                // step s_begin + p - 1 during this phase)
-                if (p >= 2) publish(s_begin + p - 2);
-                // 2) receive tile t+1's step gs = s_begin - 1 + p
                 const int gs = s_begin - 1 + p;
                 const bool want = gvalid(p);
                 const int c0 = u_lo + NW + gs;  // tile t+1's wave 0 column at step gs
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     const long long sp0 = __builtin_amdgcn_s_memtime();
                     unsigned nsp = 0;
 #endif
-                    const unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t + 1, gs, 0) + e0;
+                    const unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t + 1, gs, 0) + eg;
                     for (unsigned spins = 1;; ++spins) {
                         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
@@ -285,7 +297,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
             for (int q = 0; q < CR; ++q)
                 if (p0 + q < np) phase(q, p0 + q);
-            publish(s_end - 1);  // the tile's last step, after its barrier
             continue;
         }
 
@@ -469,17 +480,17 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_GRID")) a.grid = atoi(e) > 0 && atoi(e) < a.grid ? atoi(e) : a.grid;
 #endif
-    const dim3 grid(a.grid), block(64 * (kSlantNW + 1));
+    const dim3 grid(a.grid), block(64 * (kSlantNW + 2));
     constexpr int PF4 = UP ? 4 : 8, PF = UP ? 8 : 16;
     size_t pad = 0;
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_LDSPAD")) pad = (size_t)atoi(e) * 1024;
 #endif
-    if (g.D == 32) slant_kernel<UP, 1, false, kSlantNW, PF, 3><<<grid, block, pad, st>>>(a, g);
-    else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 3><<<grid, block, pad, st>>>(a, g);
-    else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 3><<<grid, block, pad, st>>>(a, g);
+    if (g.D == 32) slant_kernel<UP, 1, false, kSlantNW, PF, 8><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 8><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 6><<<grid, block, pad, st>>>(a, g);
 #ifndef SLANT_CR4
-#define SLANT_CR4 2
+#define SLANT_CR4 4
 #endif
     else slant_kernel<UP, 4, true, kSlantNW, PF4, SLANT_CR4><<<grid, block, 0, st>>>(a, g);
     return hipGetLastError();

@@ -6,8 +6,8 @@ SGM parameters the C-ABI exposes beyond the reference's constants -- P1, P2
 the LR threshold (inc/Solver.h:16: 1).  The oracle (oracle/sgm_oracle.c)
 takes the same parameters.  Every case runs with both bodies of the diagonal
 L8 sweep (SGM_SWEEP_SPLIT: the one-wave sweep and the memory-wave + DP-wave
-split, which the library picks by volume size), and once more in bands
-(SGM_BAND_ROWS; with and without the forward bands, SGM_FWD_BANDS)."""
+split, which the library picks by volume size), in bands (SGM_BAND_ROWS) and
+through the slanted-tile passes (SGM_SLANT)."""
 from __future__ import annotations
 
 import numpy as np
@@ -50,25 +50,14 @@ def test_random_frame(c, split, monkeypatch):
 
 
 @pytest.mark.parametrize("c", CASES, ids=[f"{c['h']}x{c['w']}_D{c['D']}_s{c['s']}_V{c['views']}" for c in CASES])
-@pytest.mark.parametrize("fwd", ["1", "0", "mixed", "t56"], ids=["fwdbands", "bwdbands", "mixed", "t56"])
-def test_random_frame_banded(c, fwd, monkeypatch):
-    """16-row bands (the schedule of volumes above the Infinity Cache): the
-    forward phase (vfwd, L5, L6) band by band top down, both views' H pairs
-    in one launch, then the backward phase (stage B's diagonal pair, L8 and
-    the final pass) band by band bottom up, chain and filter states carried
-    across band edges; SGM_FWD_BANDS=0 keeps the forward phase whole,
-    "mixed" runs 16-row forward bands with 32-row backward bands, and "t56"
-    the SGM_T56 variant (L5, L6 sweeps forming T56 in the forward bands, L7 a
-    plain sweep in the backward bands)."""
-    monkeypatch.setenv("SGM_BAND_ROWS", "16")
-    if fwd == "t56":  # SGM_T56: T56 = L5 + L6 in the forward bands, L7 a plain sweep
-        monkeypatch.setenv("SGM_T56", "1")
-        fwd = "1"
-    if fwd == "mixed":  # forward and backward bands of different sizes
-        monkeypatch.setenv("SGM_BAND_ROWS", "32")
-        monkeypatch.setenv("SGM_FWD_BAND_ROWS", "16")
-        fwd = "1"
-    monkeypatch.setenv("SGM_FWD_BANDS", fwd)
+@pytest.mark.parametrize("rows", ["16", "32"])
+def test_random_frame_banded(c, rows, monkeypatch):
+    """Bands (the schedule of volumes above the Infinity Cache): the forward
+    phase (vfwd, L5, L6) band by band top down, both views' H pairs in one
+    launch, then the backward phase (stage B's diagonal pair, L8 and the final
+    pass) band by band bottom up, chain and filter states carried across band
+    edges."""
+    monkeypatch.setenv("SGM_BAND_ROWS", rows)
     _check(c)
 
 

@@ -1,13 +1,13 @@
-"""The frame schedule's variants give the same maps bit for bit.
+"""The frame schedules give the same maps bit for bit.
 
-run_frame (sgm_capi.hip) picks between launch groupings that must not change
-results: both views' DSI + horizontal IIR in one launch (cost_h2_kernel) or
-one launch per view, and -- for volumes above the 256 MB Infinity Cache --
-both views' final passes in one launch (pair_final2_kernel) or one per view.
-SGM_CONCURRENT_VIEWS=1 (read at sgm_create) runs the right view on a second
-stream with per-view launches; SGM_SPLIT_FINAL=1 (read per frame) keeps the
-per-view final passes; SGM_SUB_CM=0 keeps row-major sub-pixel maps.  The default schedule is pinned against the oracle by
-test_gpu_parity.py / test_gpu_fullsize.py; these tests pin the variants to it.
+run_frame (sgm_capi.hip) picks the schedule by volume size: joint two-view
+launches when both cost volumes fit the 256 MB Infinity Cache together,
+per-view whole-volume passes below 256 MB per view, bands above it
+(SGM_BAND_ROWS overrides the band size, 0 = whole-volume passes and the joint
+final launch), and the slanted-tile passes (SGM_SLANT=1, sgm_slant.hip).  The
+default schedule is pinned against the oracle by test_gpu_parity.py /
+test_gpu_fullsize.py; these tests pin the others to it at sizes where the
+library would not pick them.
 """
 from __future__ import annotations
 
@@ -48,35 +48,24 @@ def _same(a, b):
     (120, 330, 64, False, False),
     (96, 260, 128, True, True),
     (80, 240, 256, True, True),
-    (100, 300, 64, True, False),   # one mask only: per-view cost launches either way
+    (100, 300, 64, True, False),   # one mask only: per-view cost launches
     (375, 1242, 128, True, True),
 ])
-def test_joint_cost_launch_matches_per_view(h, w, D, sky_l, sky_r):
-    _same(_run(h, w, D, sky_l, sky_r, {}), _run(h, w, D, sky_l, sky_r, {"SGM_CONCURRENT_VIEWS": "1"}))
+@pytest.mark.parametrize("env", [{"SGM_BAND_ROWS": "16"}, {"SGM_BAND_ROWS": "32"}, {"SGM_SLANT": "1"}],
+                         ids=["bands16", "bands32", "slant"])
+def test_schedules_match_default(h, w, D, sky_l, sky_r, env):
+    _same(_run(h, w, D, sky_l, sky_r, {}), _run(h, w, D, sky_l, sky_r, env))
 
 
-def test_joint_final_matches_per_view():
+def test_whole_volume_joint_final_matches_bands():
     # 512 x 1056 x 128 f32 = 277 MB per volume: above the Infinity Cache, so
-    # the whole-volume schedule (SGM_BAND_ROWS=0: pair_final2_kernel is the
-    # unbanded schedule's joint final launch) runs both final passes as one
-    # launch; SGM_SPLIT_FINAL=1 runs one per view
+    # the default runs bands; SGM_BAND_ROWS=0 runs whole-volume passes with
+    # both views' final passes in one launch (pair_final2_kernel)
     h, w, D = 512, 1056, 128
     assert h * w * D * 4 > 256 * 1024 * 1024
-    _same(_run(h, w, D, False, False, {"SGM_BAND_ROWS": "0"}),
-          _run(h, w, D, False, False, {"SGM_BAND_ROWS": "0", "SGM_SPLIT_FINAL": "1"}))
-
-
-@pytest.mark.parametrize("band_rows", ["16", "0"])
-def test_banded_concurrent_views_match_default(band_rows):
-    # SGM_CONCURRENT_VIEWS=1 on a banded frame: each view runs its forward
-    # bands, its own H pair and its backward bands on its own stream with
-    # per-view carries (run_frame's split_h = false path); against the
-    # default single-stream schedule of the same bands
-    h, w, D = 200, 640, 128
-    env = {"SGM_BAND_ROWS": band_rows}
-    _same(_run(h, w, D, True, True, env), _run(h, w, D, True, True, dict(env, SGM_CONCURRENT_VIEWS="1")))
-    _same(_run(h, w, D, False, True, env),
-          _run(h, w, D, False, True, dict(env, SGM_CONCURRENT_VIEWS="1", SGM_FWD_BANDS="0")))
+    base = _run(h, w, D, False, False, {})
+    _same(base, _run(h, w, D, False, False, {"SGM_BAND_ROWS": "0"}))
+    _same(base, _run(h, w, D, False, False, {"SGM_SLANT": "1"}))
 
 
 CROSS_STREAM = r"""
@@ -137,12 +126,3 @@ def test_calls_on_different_streams_are_ordered():
     r = subprocess.run([sys.executable, "-c", CROSS_STREAM, root], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "cross-stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-
-
-@pytest.mark.parametrize("h,w,D,sky", [(120, 330, 64, False), (200, 640, 128, True),
-                                       (72, 200, 256, True), (375, 1242, 128, False)])
-def test_column_major_sub_maps_match_row_major(h, w, D, sky):
-    # two-view frames write their sub-pixel maps column-major (whole cache lines
-    # from the final pass's one-column workgroups) and lr_cm_kernel transposes
-    # through LDS; SGM_SUB_CM=0 keeps row-major maps and lr_kernel
-    _same(_run(h, w, D, sky, sky, {}), _run(h, w, D, sky, sky, {"SGM_SUB_CM": "0"}))
