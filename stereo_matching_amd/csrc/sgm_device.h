@@ -26,6 +26,18 @@ __device__ __forceinline__ int tid_x() { return (int)__builtin_amdgcn_workitem_i
 // must be a uniform branch, not an exec-masked one)
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(tid_x() >> 6); }
 
+// Block b -> column so that each XCD takes one contiguous range of columns.
+// Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one;
+// MI355X_MICROARCH.md "Workgroup dispatch"), so the plain b -> column map puts
+// neighbouring columns on different XCDs, and a row-major output row's 128-B
+// line is written 4 bytes at a time from 8 L2s, each writing back its own
+// partial line.  With this map the 32 columns of a line share one L2, which
+// merges their stores before the line leaves.  A bijection on [0, n).
+__device__ __forceinline__ int xcd_column(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // Hamming distance of two census words as an exact float.  Two 32-bit counts

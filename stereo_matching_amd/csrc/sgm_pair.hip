@@ -63,8 +63,14 @@ template <int V, bool FULL, bool BAND = false>
 __global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
     __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
+#ifdef SGM_NO_XCD_COLUMNS
+    const int path = bid_x();
+#else
+    // row-major output maps (one-view frames): a line's columns on one XCD
+    const int path = a.sub_cm ? bid_x() : xcd_column(bid_x(), g.W);
+#endif
     pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>(), BAND>(
-        a, g, bid_x(), wave_id(), lds.s, &lds);
+        a, g, path, wave_id(), lds.s, &lds);
 }
 
 // Both views' final passes in one launch (workgroup z = view).  Above the

@@ -69,8 +69,10 @@ __device__ __forceinline__ unsigned long long granule(float x, unsigned tag) {
     const unsigned b = __float_as_uint(x), t = tag << 16;
     return ((unsigned long long)(t | (b >> 16)) << 32) | (t | (b & 0xffffu));
 }
-__device__ __forceinline__ bool granule_ok(unsigned long long q, unsigned tag) {
-    return (unsigned)(q >> 48) == tag && ((unsigned)q >> 16) == tag;
+// (bitwise, no short circuit: a branch here would make the waitcnt pass
+// drain every load in flight before the next use of the ring)
+__device__ __forceinline__ unsigned granule_ok(unsigned long long q, unsigned tag) {
+    return (unsigned)((unsigned)(q >> 48) == tag) & (unsigned)(((unsigned)q >> 16) == tag);
 }
 __device__ __forceinline__ float granule_value(unsigned long long q) {
     return __uint_as_float(((unsigned)(q >> 16) & 0xffff0000u) | ((unsigned)q & 0xffffu));
@@ -175,13 +177,33 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                     if (dact) store_granules<V>(gb + x * D, y, tag);
                 }
             };
-            lds_barrier();
-            if (nsteps >= 1) lds_barrier();
+#ifdef SGM_SLANT_STAMPS
+            long long pw = 0, pb = 0, pt = __builtin_amdgcn_s_memtime();
+#define PUB_BAR()                                              \
+    {                                                          \
+        const long long t0_ = __builtin_amdgcn_s_memtime();    \
+        pw += t0_ - pt;                                        \
+        lds_barrier();                                         \
+        pt = __builtin_amdgcn_s_memtime();                     \
+        pb += pt - t0_;                                        \
+    }
+#else
+#define PUB_BAR() lds_barrier()
+#endif
+            PUB_BAR();
+            if (nsteps >= 1) PUB_BAR();
             for (int p = 2; p <= nsteps; ++p) {
                 publish(s_begin + p - 2);
-                lds_barrier();
+                PUB_BAR();
             }
+#undef PUB_BAR
             publish(s_end - 1);
+#ifdef SGM_SLANT_STAMPS
+            if (lane == 0) {
+                SLANT_STAMP(12, pw);
+                SLANT_STAMP(13, pb);
+            }
+#endif
             continue;
         }
         if (wave == NW) {
@@ -219,6 +241,9 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
             };
 #pragma unroll
             for (int q = 0; q < CR; ++q) issue(q, q);
+#ifdef SGM_SLANT_STAMPS
+            long long rw = 0, rb = 0, rt = __builtin_amdgcn_s_memtime();
+#endif
             auto phase = [&](int slot, int p) {
                 const int gs = s_begin - 1 + p;
                 const bool want = gvalid(p);
@@ -229,18 +254,25 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                     const int c = c0 + X::wave(x);
                     need[x] = want && c >= 0 && c < W;
                 }
-                auto check = [&] {
-                    bool ok = true;
+                // decode and check every granule of the slot unconditionally
+                // (bitwise flags): the ring's waits stay exact
+                float y[NX][V];
+                auto decode = [&]() -> bool {
+                    unsigned ok = 1u;
 #pragma unroll
                     for (int x = 0; x < NX; ++x)
 #pragma unroll
-                        for (int v = 0; v < V; ++v) ok &= !need[x] || granule_ok(rq[slot][x][v], tag);
+                        for (int v = 0; v < V; ++v) {
+                            const unsigned long long q = rq[slot][x][v];
+                            y[x][v] = granule_value(q);
+                            ok &= (unsigned)!need[x] | granule_ok(q, tag);
+                        }
 #if defined(SLANT_PROBE_NOWAIT) || defined(SLANT_PROBE_NOCOURIER)
-                    ok = true;  // timing probe: no hand-off wait (wrong results)
+                    ok = 1u;  // timing probe: no hand-off wait (wrong results)
 #endif
-                    return ok || !dact;
+                    return (ok | (unsigned)!dact) != 0u;
                 };
-                if (!__all(check())) {
+                if (!__all(decode())) {
                     // slow path: the next tile is not CR steps ahead
 #ifdef SGM_SLANT_STAMPS
                     const long long sp0 = __builtin_amdgcn_s_memtime();
@@ -259,7 +291,7 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
 #ifdef SGM_SLANT_STAMPS
                         nsp = spins;
 #endif
-                        if (__all(check())) break;
+                        if (__all(decode())) break;
                         if (spins >= kSlantSpinLimit) {
                             if (lane == 0) atomicOr(&ctl->err, 1u);
                             break;
@@ -278,15 +310,23 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                 const int par = gs & 1;
 #pragma unroll
                 for (int x = 0; x < NX; ++x) {
-                    float y[V];
+                    float yy[V];
 #pragma unroll
-                    for (int v = 0; v < V; ++v) y[v] = dact ? granule_value(rq[slot][x][v]) : SGM_INF;
-                    const float m = wave_min(lane_min(y));
-                    store_lds_v<V>(&L.st[par][NW + X::wave(x)][X::kind(x)][e0], y);
+                    for (int v = 0; v < V; ++v) yy[v] = dact ? y[x][v] : SGM_INF;
+                    const float m = wave_min(lane_min(yy));
+                    store_lds_v<V>(&L.st[par][NW + X::wave(x)][X::kind(x)][e0], yy);
                     if (lane == 0) L.pm[par][NW + X::wave(x)][X::kind(x)] = m;
                 }
                 issue(slot, p + CR);
+#ifdef SGM_SLANT_STAMPS
+                const long long t0_ = __builtin_amdgcn_s_memtime();
+                rw += t0_ - rt;
                 lds_barrier();
+                rt = __builtin_amdgcn_s_memtime();
+                rb += rt - t0_;
+#else
+                lds_barrier();
+#endif
             };
             const int np = nsteps + 1;
             int p0 = 0;
@@ -297,6 +337,12 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
             for (int q = 0; q < CR; ++q)
                 if (p0 + q < np) phase(q, p0 + q);
+#ifdef SGM_SLANT_STAMPS
+            if (lane == 0) {
+                SLANT_STAMP(10, rw);
+                SLANT_STAMP(11, rb);
+            }
+#endif
             continue;
         }
 

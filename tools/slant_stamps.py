@@ -35,5 +35,7 @@ cyc = 100.0  # s_memtime ticks at 100 MHz on gfx950? (printed raw too)
 print("raw:", x[:10])
 steps = max(x[0], 1)
 print(f"per tile-step (wave 0): work {x[4] / steps:.1f}  barrier {x[5] / steps:.1f} ticks")
+print(f"receiver per phase: work {x[10] / steps:.1f}  barrier {x[11] / steps:.1f}; "
+      f"publisher per phase: work {x[12] / steps:.1f}  barrier {x[13] / steps:.1f} ticks")
 print(f"inside tiles per WG: {x[7] / max(x[8], 1):.0f} ticks; courier re-polled phases {x[1]} "
       f"({x[1] / steps * 100:.1f}% of steps), re-polls {x[2]}, ticks in re-polls {x[3]}")
