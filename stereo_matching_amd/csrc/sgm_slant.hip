@@ -94,8 +94,9 @@ __device__ __forceinline__ float uni_f(float x) {
 // [2] courier re-polls  [3] courier cycles in re-polls  [4] compute wave 0
 // cycles between barriers  [5] compute wave 0 cycles in barriers
 // [7] cycles inside tiles (wave 0)  [8] workgroups  [9] tiles
-static __device__ unsigned long long slant_stamps[16];
-#define SLANT_STAMP(i, v) atomicAdd(&slant_stamps[i], (unsigned long long)(v))
+// (the top-down pass's at [0, 16), the bottom-up pass's at [16, 32))
+static __device__ unsigned long long slant_stamps[32];
+#define SLANT_STAMP(i, v) atomicAdd(&slant_stamps[(UP ? 16 : 0) + (i)], (unsigned long long)(v))
 #endif
 
 // polls before a courier gives up (a hang guard: ~seconds; SlantCtl::err is set)
@@ -359,7 +360,13 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
         const bool never = s_lo > s_hi;
         auto off_of = [&](int s) -> long long {
             const int sc = uniform(min(max(s, s_lo), s_hi));
+#ifdef SLANT_PROBE_HOT
+            // timing probe: every stream load from one small L2-resident
+            // block, every store to the dummy area (wrong results)
+            return (long long)sc * 0 + (long long)(k * 64 * V + e0) + (never ? 0 : 0);
+#else
             return never ? (long long)e0 : base + (long long)sc * dstep;
+#endif
         };
         constexpr int NS = UP ? 4 : 1;  // streams: C (+ S12, L3, T56)
         float rb[NS][PF][V];
@@ -386,6 +393,34 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
         for (int v = 0; v < V; ++v) po[v] = 0.0f;
         float mo = 0.0f;
+        // the WTA of step s runs in step s + 1, after that step's DP chains
+        // (it feeds no chain): its reductions interleave with theirs instead
+        // of lengthening the step ahead of the barrier.  ptot / pstep: the
+        // deferred step's totals and pixel (pstep < 0: none yet).
+        float ptot[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) ptot[v] = 0.0f;
+        int pstep = -1;
+        auto wta_out = [&](const float (&tt)[V], int ps) {
+            int d;
+            float f;
+#ifdef SLANT_PROBE_NOWTA
+            d = 0;  // timing probe: no WTA (wrong results)
+            f = tt[0];
+#else
+            wta_subpixel<V>(tt, D, a.uniq, d, f);
+#endif
+            // outputs: an inactive step writes the dummy words instead
+            const int j = u + ps;
+            const bool act = ps >= 0 && j >= 0 && j < W;
+            const long long pix = (long long)(H - 1 - ps) * W + j;
+            float *fs = act ? sv.sub + pix : a.dummy + 256;
+            if (lane == 0) *fs = f;
+            if (sv.disp) {
+                uint16_t *ds = act ? sv.disp + pix : reinterpret_cast<uint16_t *>(a.dummy + 257);
+                if (lane == 0) *ds = (uint16_t)d;
+            }
+        };
         lds_barrier();  // the courier's prologue phase
 #ifdef SGM_SLANT_STAMPS
         long long st_prev = __builtin_amdgcn_s_memtime(), st_work = 0, st_wait = 0;
@@ -431,30 +466,26 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
                 for (int v = 0; v < V; ++v)
                     tot[v] = ((rb[1][q][v] + rb[2][q][v]) + L4[v]) + ((rb[3][q][v] + Lo[v]) + L2[v]);
-                int d;
-                float f;
-#ifdef SLANT_PROBE_NOWTA
-                d = 0;  // timing probe: no WTA (wrong results)
-                f = tot[0];
-#else
-                wta_subpixel<V>(tot, D, a.uniq, d, f);
-#endif
                 store_lds_v<V>(&L.st[cp][k][0][e0], L4);
                 if (lane == 0) L.pm[cp][k][0] = n4;
-                // outputs: an inactive step writes the dummy words instead
-                const long long pix = (long long)(H - 1 - s) * W + j;
-                float *fs = act ? sv.sub + pix : a.dummy + 256;
-                if (lane == 0) *fs = f;
-                if (sv.disp) {
-                    uint16_t *ds = act ? sv.disp + pix : reinterpret_cast<uint16_t *>(a.dummy + 257);
-                    if (lane == 0) *ds = (uint16_t)d;
-                }
+#ifdef SLANT_WTA_INLINE
+                wta_out(tot, s);
+#else
+                wta_out(ptot, pstep);
+#pragma unroll
+                for (int v = 0; v < V; ++v) ptot[v] = tot[v];
+                pstep = s;
+#endif
             } else {
                 // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
                 float o[V];
 #pragma unroll
                 for (int v = 0; v < V; ++v) o[v] = Lo[v] + L2[v];
+#ifdef SLANT_PROBE_HOT
+                float *dst = a.dummy + e0;
+#else
                 float *dst = act ? sv.t56w + off_of(s) : a.dummy + e0;
+#endif
                 store_v_nt<V>(dst, o, dact);
             }
             store_lds_v<V>(&L.st[cp][k][K2][e0], L2);
@@ -481,6 +512,9 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
         for (int q = 0; q < PF; ++q)
             if (s0 + q < s_end) step(q, s0 + q);
+#ifndef SLANT_WTA_INLINE
+        if constexpr (UP) wta_out(ptot, pstep);
+#endif
 #ifdef SGM_SLANT_STAMPS
         if (k == 0 && lane == 0) {
             SLANT_STAMP(0, nsteps);
@@ -552,7 +586,7 @@ extern "C" int sgm_debug_slant_stamps(unsigned long long *out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sgm::slant_stamps), sizeof(sgm::slant_stamps)) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(sgm::slant_stamps), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -18,7 +18,7 @@ out = torch.empty((h, w), dtype=torch.float32, device=dev)
 sgm = SGM(h, w, 1, D, views=V, device=0)
 lib = _capi.lib()
 lib.sgm_debug_slant_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-b = (ctypes.c_ulonglong * 16)()
+b = (ctypes.c_ulonglong * 32)()
 for it in range(3):
     sgm.process_device(dl.data_ptr(), dr.data_ptr(), out.data_ptr())
     torch.cuda.synchronize()
@@ -28,14 +28,17 @@ sgm.process_device(dl.data_ptr(), dr.data_ptr(), out.data_ptr())
 torch.cuda.synchronize()
 prof = sgm.get_profile()
 lib.sgm_debug_slant_stamps(b, 1)
-x = list(b)
-print(f"{h}x{w} D={D} V={V}: slant_up {prof['slant_up'][1]:.3f} ms, slant_down {prof['slant_down'][1]:.3f} ms "
-      f"(both passes below); workgroups {x[8]}, tiles {x[9]}, tile-steps {x[0]}")
-cyc = 100.0  # s_memtime ticks at 100 MHz on gfx950? (printed raw too)
-print("raw:", x[:10])
-steps = max(x[0], 1)
-print(f"per tile-step (wave 0): work {x[4] / steps:.1f}  barrier {x[5] / steps:.1f} ticks")
-print(f"receiver per phase: work {x[10] / steps:.1f}  barrier {x[11] / steps:.1f}; "
-      f"publisher per phase: work {x[12] / steps:.1f}  barrier {x[13] / steps:.1f} ticks")
-print(f"inside tiles per WG: {x[7] / max(x[8], 1):.0f} ticks; courier re-polled phases {x[1]} "
-      f"({x[1] / steps * 100:.1f}% of steps), re-polls {x[2]}, ticks in re-polls {x[3]}")
+xa = list(b)
+print(f"{h}x{w} D={D} V={V}: slant_up {prof['slant_up'][1]:.3f} ms, slant_down {prof['slant_down'][1]:.3f} ms")
+for name, x, ms in (("down", xa[:16], prof['slant_down'][1]), ("up", xa[16:], prof['slant_up'][1])):
+    steps = max(x[0], 1)
+    wg = max(x[8], 1)
+    rate = x[7] / wg / (ms * 1e3)  # ticks per us (inside-tile ticks per WG over the launch)
+    print(f"  {name}: workgroups {x[8]}, tiles {x[9]}, tile-steps {x[0]} ({x[0] / wg:.0f} per WG), "
+          f"{ms * 1e3 / (x[0] / wg):.2f} us per step, ~{rate:.0f} ticks/us")
+    print(f"    compute wave 0 per step: work {x[4] / steps:.0f}  barrier {x[5] / steps:.0f} ticks")
+    print(f"    receiver per phase: work {x[10] / steps:.0f}  barrier {x[11] / steps:.0f}; "
+          f"publisher per phase: work {x[12] / steps:.0f}  barrier {x[13] / steps:.0f} ticks")
+    print(f"    re-polled phases {x[1]} ({x[1] / steps * 100:.1f}%), re-polls {x[2]}, "
+          f"ticks in re-polls per phase {x[3] / steps:.0f}")
+    print("    raw:", x[:14])
