@@ -325,6 +325,22 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
                  [&] { return sgm::launch_pair_bwd(fam, mode, a, h->g, st); });
 }
 
+// The slanted-tile schedule replaces the bands where every workgroup runs
+// at least two full-height tiles' worth of steps: views * W * H / (NW * CUs)
+// >= 2H.  Measured (profiles/r04_experiments/slant.txt): 4K256 with both
+// views, 49.3 vs 56.7 ms per frame; HD256 (one tile round and a bit per
+// workgroup), 14.2 vs 14.0 -- there the tile-to-tile hand-off chain, not the
+// bytes, sets the time.  Only above the Infinity Cache (the bands' domain).
+bool slant_default(Geom g, int nviews) {
+    const double vol = (double)g.W * g.H * g.D * sizeof(float);
+    if (vol <= 256.0 * 1024 * 1024) return false;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    return (long long)nviews * g.W >= 2LL * sgm::kSlantNW * cus;
+}
+
 // Rows per band of the backward phase (stage B's diagonal pair, the L8
 // sweep, the final pass) for cost volumes above the 256 MB Infinity Cache:
 // about 192 MB of cost volume per band, so that a band's C and T stay in the
@@ -972,10 +988,11 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
                 rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D * (f == 2 ? 3 : 1));
         }
         {
-            // the slanted schedule: SGM_SLANT=1/0 forces it on/off (parity
-            // tests cover it at every size); default off until measured
+            // the slanted schedule: by size (slant_default), SGM_SLANT=1/0
+            // forces it on/off (the parity tests run it at every size)
             const char *e = getenv("SGM_SLANT");
-            h->slant = !p->aux_only && p->solver == SGM_SOLVER_SGM && e && *e == '1';
+            const bool want = e && *e ? *e == '1' : slant_default(h->g, h->nviews);
+            h->slant = !p->aux_only && p->solver == SGM_SOLVER_SGM && want;
         }
         if (!rc && h->slant) {
             for (int v = 0; v < h->nviews && !rc; ++v) rc = dalloc(h, &h->d_l3[v], nvol);

@@ -78,11 +78,52 @@ __device__ __forceinline__ float granule_value(unsigned long long q) {
     return __uint_as_float(((unsigned)(q >> 16) & 0xffff0000u) | ((unsigned)q & 0xffffu));
 }
 
+// One tile's granules (H steps x 3 slots x D) as a buffer resource, moved by
+// sc1 (write-through) buffer stores and loads: 16 bytes (two granules) per
+// lane and instruction where a lane holds two or more (D >= 128), else 8.  A
+// lane's V granules as separate 8-byte sc1 stores cost ~2.7x the 16-byte
+// form per byte (MI355X_MICROARCH.md "stores of each flavour",
+// cdna_hip_programming.md Guideline 16 pitfall 7).  Two granules in one
+// 16-byte access stay independently checkable: each 4-byte half carries the
+// tag.  A resource with 0 records drops every access through it (the range
+// check): waves without exit states store through one, so every compute wave
+// runs the same instruction stream.
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
+typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
+constexpr int kGranAux = 16;           // cache policy: sc1
+constexpr int kGranOff = 0x40000000;   // an offset past every tile's records
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(unsigned long long *tile_base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, bytes, 0x00020000);
+}
 template <int V>
-__device__ __forceinline__ void store_granules(unsigned long long *g, const float (&x)[V], unsigned tag) {
+__device__ __forceinline__ void store_granules(__amdgpu_buffer_rsrc_t rs, int off, const float (&x)[V],
+                                               unsigned tag) {
+    if constexpr (V == 1) {
+        const unsigned long long g0 = granule(x[0], tag);
+        const v2u32 q = {(unsigned)g0, (unsigned)(g0 >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b64(q, rs, off, 0, kGranAux);
+    } else {
 #pragma unroll
-    for (int v = 0; v < V; ++v)
-        __hip_atomic_store(g + v, granule(x[v], tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int v = 0; v < V; v += 2) {
+            const unsigned long long g0 = granule(x[v], tag), g1 = granule(x[v + 1], tag);
+            const v4u32 q = {(unsigned)g0, (unsigned)(g0 >> 32), (unsigned)g1, (unsigned)(g1 >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b128(q, rs, off + v * 8, 0, kGranAux);
+        }
+    }
+}
+template <int V>
+__device__ __forceinline__ void load_granules(unsigned long long (&g)[V], __amdgpu_buffer_rsrc_t rs, int off) {
+    if constexpr (V == 1) {
+        const v2u32 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, kGranAux);
+        g[0] = ((unsigned long long)q[1] << 32) | q[0];
+    } else {
+#pragma unroll
+        for (int v = 0; v < V; v += 2) {
+            const v4u32 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + v * 8, 0, kGranAux);
+            g[v] = ((unsigned long long)q[1] << 32) | q[0];
+            g[v + 1] = ((unsigned long long)q[3] << 32) | q[2];
+        }
+    }
 }
 
 __device__ __forceinline__ float uni_f(float x) {
@@ -121,7 +162,7 @@ struct SlantExits {
 // rings stay in flight across steps (a branch around a memory instruction
 // makes later waits drain everything outstanding).
 template <bool UP, int V, bool FULL, int NW, int PF, int CR>
-__global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom g) {
+__global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom g) {
     constexpr int NE = UP ? 2 : 1;         // states exchanged per wave
     constexpr int K2 = UP ? 1 : 0;         // index of the wave k+2 family (L8 / L6)
     using X = SlantExits<UP>;
@@ -131,9 +172,10 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
     const int H = g.H, W = g.W, D = g.D;
     const int e0 = lane * V;
     const bool dact = FULL || e0 < D;
-    // granule offset of this lane: lanes past D (D = 32) read lane 0's and
-    // store nothing (their e0 would run into the next slot)
-    const int eg = dact ? e0 : 0;
+    // byte offset of this lane's granules in a slot: lanes past D (D = 32)
+    // get one past the buffer's records (their loads read 0, stores drop)
+    const int goff = dact ? e0 * 8 : kGranOff;
+    const int tile_bytes = H * 3 * D * 8;
     const int T = a.ntiles, total = T * a.nviews;
     SlantCtl *ctl = a.ctl + (UP ? 1 : 0);
     // one step: up-right (-W*D + D) bottom-up, down-right (W*D + D) top-down
@@ -160,53 +202,6 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
         const int s_end = min(H, W - u_lo);
         const int nsteps = s_end - s_begin;
 
-        if (wave == NW + 1) {
-            // ---------------------------------------------- publisher wave
-            // Phase p (p = 0 .. nsteps, each ending on the tile's barrier)
-            // publishes this tile's exit states of step s_begin + p - 2,
-            // which waves 0 and 1 wrote to LDS in the step that ended at the
-            // previous barrier (the compute waves run step s_begin + p - 1
-            // meanwhile); the last step goes out after the last barrier.
-            // Stores only: its waits never hold the receiver's loads.
-            auto publish = [&](int sp) {
-                const int par = sp & 1;
-                unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t, sp, 0) + eg;
-#pragma unroll
-                for (int x = 0; x < NX; ++x) {
-                    float y[V];
-                    load_lds_v<V>(y, &L.st[par][X::wave(x)][X::kind(x)][e0]);
-                    if (dact) store_granules<V>(gb + x * D, y, tag);
-                }
-            };
-#ifdef SGM_SLANT_STAMPS
-            long long pw = 0, pb = 0, pt = __builtin_amdgcn_s_memtime();
-#define PUB_BAR()                                              \
-    {                                                          \
-        const long long t0_ = __builtin_amdgcn_s_memtime();    \
-        pw += t0_ - pt;                                        \
-        lds_barrier();                                         \
-        pt = __builtin_amdgcn_s_memtime();                     \
-        pb += pt - t0_;                                        \
-    }
-#else
-#define PUB_BAR() lds_barrier()
-#endif
-            PUB_BAR();
-            if (nsteps >= 1) PUB_BAR();
-            for (int p = 2; p <= nsteps; ++p) {
-                publish(s_begin + p - 2);
-                PUB_BAR();
-            }
-#undef PUB_BAR
-            publish(s_end - 1);
-#ifdef SGM_SLANT_STAMPS
-            if (lane == 0) {
-                SLANT_STAMP(12, pw);
-                SLANT_STAMP(13, pb);
-            }
-#endif
-            continue;
-        }
         if (wave == NW) {
             // ----------------------------------------------- receiver wave
             // Phase p = 0 .. nsteps (the prologue, then one per step; each
@@ -218,32 +213,25 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
             auto gvalid = [&](int p) {
                 return t + 1 < T && (p >= 1 || s_begin >= 1) && p < nsteps;
             };
-            // granules of (tile t+1, step s_begin - 1 + p); a phase with
-            // nothing to fetch loads (and ignores) this tile's first step's,
-            // so every load stays inside the buffer
-            auto gsrc = [&](int p) -> const unsigned long long * {
-                const bool ok = gvalid(p);
-                const int tt = uniform(ok ? t + 1 : t);
-                const int ss = uniform(ok ? s_begin - 1 + p : s_begin);
-                return sv.gran + gran_index(T, H, D, view, tt, ss, 0) + eg;
-            };
+            // granules of (tile t+1, step s_begin - 1 + p), through tile
+            // t+1's resource; a phase with nothing to fetch loads (and
+            // ignores) step s_begin's, and the last tile reads its own
+            const auto rrs = gran_rsrc(sv.gran + gran_index(T, H, D, view, t + 1 < T ? t + 1 : t, 0, 0), tile_bytes);
+            auto gstep = [&](int p) { return uniform(gvalid(p) ? s_begin - 1 + p : s_begin); };
             unsigned long long rq[CR][NX][V];
             auto issue = [&](int slot, int p) {
 #ifdef SLANT_PROBE_NOCOURIER
                 return;  // timing probe: no hand-off loads (wrong results)
 #endif
-                const unsigned long long *gb = gsrc(p);
+                const int ss = gstep(p);
 #pragma unroll
-                for (int x = 0; x < NX; ++x)
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        rq[slot][x][v] = __hip_atomic_load(const_cast<unsigned long long *>(gb + x * D + v),
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int x = 0; x < NX; ++x) load_granules<V>(rq[slot][x], rrs, (ss * 3 + x) * D * 8 + goff);
             };
 #pragma unroll
             for (int q = 0; q < CR; ++q) issue(q, q);
 #ifdef SGM_SLANT_STAMPS
             long long rw = 0, rb = 0, rt = __builtin_amdgcn_s_memtime();
+            long long rp_phases = 0, rp_polls = 0, rp_ticks = 0;  // added once per tile
 #endif
             auto phase = [&](int slot, int p) {
                 const int gs = s_begin - 1 + p;
@@ -279,16 +267,12 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                     const long long sp0 = __builtin_amdgcn_s_memtime();
                     unsigned nsp = 0;
 #endif
-                    const unsigned long long *gb = sv.gran + gran_index(T, H, D, view, t + 1, gs, 0) + eg;
                     for (unsigned spins = 1;; ++spins) {
                         __builtin_amdgcn_s_sleep(1);
+                        // (a compiler barrier: the re-poll loads stay inside the loop)
+                        asm volatile("" ::: "memory");
 #pragma unroll
-                        for (int x = 0; x < NX; ++x)
-#pragma unroll
-                            for (int v = 0; v < V; ++v)
-                                rq[slot][x][v] = __hip_atomic_load(
-                                    const_cast<unsigned long long *>(gb + x * D + v), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+                        for (int x = 0; x < NX; ++x) load_granules<V>(rq[slot][x], rrs, (gs * 3 + x) * D * 8 + goff);
 #ifdef SGM_SLANT_STAMPS
                         nsp = spins;
 #endif
@@ -299,11 +283,9 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                         }
                     }
 #ifdef SGM_SLANT_STAMPS
-                    if (lane == 0) {
-                        SLANT_STAMP(1, 1);
-                        SLANT_STAMP(2, nsp);
-                        SLANT_STAMP(3, __builtin_amdgcn_s_memtime() - sp0);
-                    }
+                    rp_phases += 1;
+                    rp_polls += nsp;
+                    rp_ticks += __builtin_amdgcn_s_memtime() - sp0;
 #endif
                 }
                 // (a phase with nothing wanted writes slots that no valid
@@ -342,6 +324,9 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
             if (lane == 0) {
                 SLANT_STAMP(10, rw);
                 SLANT_STAMP(11, rb);
+                SLANT_STAMP(1, rp_phases);
+                SLANT_STAMP(2, rp_polls);
+                SLANT_STAMP(3, rp_ticks);
             }
 #endif
             continue;
@@ -350,6 +335,14 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
         // ------------------------------------------------- compute waves
         const int k = wave;
         const int u = u_lo + k;
+        // exit states (this tile's waves 0 and 1, read by tile t-1's
+        // receiver): stored as granules right after each step's DP.  Bottom-
+        // up, wave 0 stores L4 (slot 0) and L8 (slot 1), wave 1 L8 (slot 2);
+        // top-down, wave k < 2 stores L6 (slot k).  The other waves store
+        // through a resource with no records (dropped).
+        const auto xrs_a = gran_rsrc(sv.gran + gran_index(T, H, D, view, t, 0, 0), k < 2 ? tile_bytes : 0);
+        const auto xrs_b = gran_rsrc(sv.gran + gran_index(T, H, D, view, t, 0, 0), UP && k == 0 ? tile_bytes : 0);
+        const int xslot_a = UP ? (k == 0 ? 0 : 2) : (k < 2 ? k : 0);
         // pixel of step s: row H-1-s (bottom-up) or s (top-down), column u+s.
         // Steps where this wave's pixel lies outside the image load a clamped
         // (valid) pixel, store to the dummy area, and their states are never
@@ -460,6 +453,13 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                 m1 = v1 ? m1 : 0.0f;
                 float L4[V];
                 dp_step<V>(q1, m1, c, L4, a.p1, p2v);
+                {
+                    float xa[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v) xa[v] = k == 0 ? L4[v] : L2[v];
+                    store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, xa, tag);
+                    store_granules<V>(xrs_b, (s * 3 + 1) * D * 8 + goff, L2, tag);
+                }
                 const float n4 = wave_min(lane_min(L4));
                 // ((S12 + L3) + L4) + ((T56 + L7) + L8)
                 float tot[V];
@@ -477,6 +477,7 @@ __global__ __launch_bounds__(64 * (NW + 2)) void slant_kernel(SlantArgs a, Geom 
                 pstep = s;
 #endif
             } else {
+                store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, L2, tag);
                 // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
                 float o[V];
 #pragma unroll
@@ -560,8 +561,17 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_GRID")) a.grid = atoi(e) > 0 && atoi(e) < a.grid ? atoi(e) : a.grid;
 #endif
-    const dim3 grid(a.grid), block(64 * (kSlantNW + 2));
-    constexpr int PF4 = UP ? 4 : 8, PF = UP ? 8 : 16;
+    const dim3 grid(a.grid), block(64 * (kSlantNW + 1));
+#ifndef SLANT_PF_UP4
+#define SLANT_PF_UP4 4
+#endif
+#ifndef SLANT_PF_DN4
+#define SLANT_PF_DN4 8
+#endif
+    // (the hand-off loads of the receiver queue behind the compute waves'
+    // stream loads in the CU's memory pipeline: deeper rings hide more
+    // stream latency but lengthen every tile-to-tile hop)
+    constexpr int PF4 = UP ? SLANT_PF_UP4 : SLANT_PF_DN4, PF = UP ? 8 : 16;
     size_t pad = 0;
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_LDSPAD")) pad = (size_t)atoi(e) * 1024;
