@@ -43,6 +43,13 @@ def short(name):
             args = name[name.index(key) + len(key):].split(">")[0].split(", ")
             if len(args) == 3 and args[2] == flag:
                 return val
+    # the slanted passes, and vfwd writing the whole L3 volume (template L3OUT)
+    if "slant_kernel<" in name:
+        return "slant_up" if name.split("slant_kernel<")[1].startswith("true") else "slant_down"
+    if "vfwd_kernel<" in name:
+        args = name[name.index("vfwd_kernel<") + len("vfwd_kernel<"):].split(">")[0].split(", ")
+        if len(args) >= 6 and args[5] == "true":
+            return "vfwd_l3"
     for key, val in NAMES:
         if key in name:
             return val
