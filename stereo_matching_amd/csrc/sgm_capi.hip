@@ -325,20 +325,24 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
                  [&] { return sgm::launch_pair_bwd(fam, mode, a, h->g, st); });
 }
 
-// The slanted-tile schedule replaces the bands where every workgroup runs
-// at least two full-height tiles' worth of steps: views * W * H / (NW * CUs)
-// >= 2H.  Measured (profiles/r04_experiments/slant.txt): 4K256 with both
-// views, 49.3 vs 56.7 ms per frame; HD256 (one tile round and a bit per
-// workgroup), 14.2 vs 14.0 -- there the tile-to-tile hand-off chain, not the
-// bytes, sets the time.  Only above the Infinity Cache (the bands' domain).
+// The slanted-tile schedule replaces the bands (above the Infinity Cache)
+// where it was measured faster (tools/slant_sizes.py,
+// profiles/r04_experiments/slant.txt): at D = 256 once every workgroup gets a
+// full-height tile's worth of steps, views * W * H / (NW * CUs) >= H (HD256
+// two views -13.9%, 4K256 one view -14.2%, two views -19%; HD256 one view
+// +12.9%, 720p D = 256 two views +3.0%); at D = 128 from two tiles per
+// workgroup (4K128 two views -4.9%; HD128 -2.4%); never at D = 64 (HD64 two
+// views +19.5%).  Below those sizes the tile-to-tile hand-off chain, not the
+// bytes, sets the passes' time.
 bool slant_default(Geom g, int nviews) {
     const double vol = (double)g.W * g.H * g.D * sizeof(float);
-    if (vol <= 256.0 * 1024 * 1024) return false;
+    if (vol <= 256.0 * 1024 * 1024 || g.D < 128) return false;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    return (long long)nviews * g.W >= 2LL * sgm::kSlantNW * cus;
+    const long long tiles_per_wg = g.D >= 256 ? 1 : 2;
+    return (long long)nviews * g.W >= tiles_per_wg * sgm::kSlantNW * cus;
 }
 
 // Rows per band of the backward phase (stage B's diagonal pair, the L8

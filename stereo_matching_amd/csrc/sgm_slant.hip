@@ -83,7 +83,8 @@ __device__ __forceinline__ float granule_value(unsigned long long q) {
 // lane and instruction where a lane holds two or more (D >= 128), else 8.  A
 // lane's V granules as separate 8-byte sc1 stores cost ~2.7x the 16-byte
 // form per byte (MI355X_MICROARCH.md "stores of each flavour",
-// cdna_hip_programming.md Guideline 16 pitfall 7).  Two granules in one
+// cdna_hip_programming.md Guideline 16 pitfall 7).  A slot's D granules sit
+// in access order: instruction k (of V/2) of lane l at byte (64k + l) * 16.  Two granules in one
 // 16-byte access stay independently checkable: each 4-byte half carries the
 // tag.  A resource with 0 records drops every access through it (the range
 // check): waves without exit states store through one, so every compute wave
@@ -107,7 +108,7 @@ __device__ __forceinline__ void store_granules(__amdgpu_buffer_rsrc_t rs, int of
         for (int v = 0; v < V; v += 2) {
             const unsigned long long g0 = granule(x[v], tag), g1 = granule(x[v + 1], tag);
             const v4u32 q = {(unsigned)g0, (unsigned)(g0 >> 32), (unsigned)g1, (unsigned)(g1 >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b128(q, rs, off + v * 8, 0, kGranAux);
+            __builtin_amdgcn_raw_buffer_store_b128(q, rs, off + (v / 2) * 1024, 0, kGranAux);
         }
     }
 }
@@ -119,7 +120,7 @@ __device__ __forceinline__ void load_granules(unsigned long long (&g)[V], __amdg
     } else {
 #pragma unroll
         for (int v = 0; v < V; v += 2) {
-            const v4u32 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + v * 8, 0, kGranAux);
+            const v4u32 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + (v / 2) * 1024, 0, kGranAux);
             g[v] = ((unsigned long long)q[1] << 32) | q[0];
             g[v + 1] = ((unsigned long long)q[3] << 32) | q[2];
         }
@@ -174,7 +175,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
     const bool dact = FULL || e0 < D;
     // byte offset of this lane's granules in a slot: lanes past D (D = 32)
     // get one past the buffer's records (their loads read 0, stores drop)
-    const int goff = dact ? e0 * 8 : kGranOff;
+    // (V = 4: granule pair k of lane l at byte (k * 64 + l) * 16 of the
+    // slot, so each 16-byte access instruction covers 1 KB contiguously --
+    // lane-contiguous pairs would leave every 32-byte sector half written
+    // per instruction, and the write-through sends each half on its own)
+    const int goff = dact ? (V == 1 ? lane * 8 : lane * 16) : kGranOff;
     const int tile_bytes = H * 3 * D * 8;
     const int T = a.ntiles, total = T * a.nviews;
     SlantCtl *ctl = a.ctl + (UP ? 1 : 0);
