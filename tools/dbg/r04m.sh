@@ -1,0 +1,3 @@
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/r04m_pytest_gpu.log 2>&1; tail -3 gpurun_out/r04m_pytest_gpu.log
+GIT_SHA=$1 bash tools/round.sh r04m bench || exit 1
+bash tools/ab.sh 4k256 1 stereo_matching_amd/libsgm_hip.so build/hpf8/libsgm_hip.so build/hpf24/libsgm_hip.so
