@@ -14,9 +14,10 @@
 // one wave, and the other two families (L4 straight up, L8 up-left) move to
 // LOWER wave numbers: L4 from wave k+1, L8 from wave k+2 of the previous
 // step.  Waves exchange them through LDS; the last one or two waves of a tile
-// take them from the next tile (t+1), whose first waves publish them as
-// 8-byte tagged granules (no flag, no fence: the data is the flag,
-// cdna_hip_programming.md Guideline 16, R2).  All dependencies point from
+// take them from the next tile (t+1), whose waves 0 and 1 store them after
+// each step as self-tagged 8-byte granules (16-byte sc1 stores of two; no
+// flag, no fence: the data is the flag, cdna_hip_programming.md Guideline 16,
+// R2), polled by this tile's receiver wave.  All dependencies point from
 // tile t+1 to tile t, so tiles claimed in the order t = T-1, T-2, ... never
 // wait on a tile no workgroup holds: no deadlock for any grid size, and a
 // tile may run any number of steps behind its right neighbour.
@@ -42,7 +43,7 @@ namespace sgm {
 // Per-step LDS exchange of one tile: the exchanged chain states (NE per wave:
 // bottom-up L4 and L8, top-down L6) and their minima, for the previous step
 // (parity (s-1)&1) and this one (s&1); slots NW and NW+1 hold the next tile's
-// wave 0 / wave 1 states, put there by the courier wave.
+// wave 0 / wave 1 states, put there by the receiver wave.
 template <int V, int NW, int NE>
 struct SlantLds {
     float st[2][NW + 2][NE][64 * V];
@@ -132,8 +133,8 @@ __device__ __forceinline__ float uni_f(float x) {
 }
 
 #ifdef SGM_SLANT_STAMPS
-// [0] tile-steps (compute wave 0)  [1] courier phases that re-polled
-// [2] courier re-polls  [3] courier cycles in re-polls  [4] compute wave 0
+// [0] tile-steps (compute wave 0)  [1] receiver phases that re-polled
+// [2] receiver re-polls  [3] receiver cycles in re-polls  [4] compute wave 0
 // cycles between barriers  [5] compute wave 0 cycles in barriers
 // [7] cycles inside tiles (wave 0)  [8] workgroups  [9] tiles
 // (the top-down pass's at [0, 16), the bottom-up pass's at [16, 32))
@@ -141,7 +142,7 @@ static __device__ unsigned long long slant_stamps[32];
 #define SLANT_STAMP(i, v) atomicAdd(&slant_stamps[(UP ? 16 : 0) + (i)], (unsigned long long)(v))
 #endif
 
-// polls before a courier gives up (a hang guard: ~seconds; SlantCtl::err is set)
+// polls before the receiver gives up (a hang guard: ~seconds; SlantCtl::err is set)
 constexpr unsigned kSlantSpinLimit = 1u << 22;
 
 // Exit states of a tile per step, as (wave, exchanged-state index) pairs:
@@ -154,7 +155,7 @@ struct SlantExits {
 };
 
 // PF: steps of data loads in flight per compute wave; CR: phases of hand-off
-// granule loads in flight in the courier.
+// granule loads in flight in the receiver.
 //
 // Memory-instruction hygiene (as the other passes): every
 // load and store of the steady-state loops is unconditional -- load
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 if (lane == 0) *ds = (uint16_t)d;
             }
         };
-        lds_barrier();  // the courier's prologue phase
+        lds_barrier();  // the receiver's prologue phase
 #ifdef SGM_SLANT_STAMPS
         long long st_prev = __builtin_amdgcn_s_memtime(), st_work = 0, st_wait = 0;
         const long long tile_t0 = st_prev;
