@@ -25,7 +25,9 @@ NAMES = [("hpair_kernel", "stage_a_h"), ("stage_a_kernel", "stage_a"), ("stage_b
          ("cc_merge_kernel", "post_cc_merge"), ("cc_count_kernel", "post_cc_count"),
          ("cc_apply_kernel", "post_cc_apply"), ("pf_prep_kernel", "post_prep"),
          ("lk_refine_kernel", "lk_refine"), ("sky_columns_kernel", "sky_columns"),
-         ("sky_gray_kernel", "sky_gray"), ("bm_wta_kernel", "bm_wta")]
+         ("sky_gray_kernel", "sky_gray"), ("bm_wta_kernel", "bm_wta"),
+         # joint two-view launches (K64)
+         ("stage_a2_kernel", "stage_a"), ("stage_b2_kernel", "stage_b"), ("sweep2_kernel<7", "sweep_L8_acc")]
 
 
 def short(name):
