@@ -68,6 +68,8 @@ struct sgm_handle {
     float *d_pf_snap;     // per median tile: the working-map cells it last read
     int *d_pf_changes;    // per median launch: tiles that changed a pixel
     int *h_pf_changes;    // pinned readback of one counter
+    unsigned *h_slant_err;  // slant: host-mapped hang-guard word (SlantArgs::err_host)
+    unsigned *d_slant_err;  //   its device-side address
     int pf_iters;         // median launches of the last post filter
     float *d_lk_in;       // LKRefine input copy (the kernel refines the map in place)
     uint8_t *d_sky_scratch;  // sky detector scratch (sgm_sky.hip)
@@ -231,6 +233,8 @@ void free_all(sgm_handle *h) {
     (void)hipFree(h->d_cloud_counts);
     if (h->h_pf_changes) (void)hipHostFree(h->h_pf_changes);
     h->h_pf_changes = nullptr;
+    if (h->h_slant_err) (void)hipHostFree(h->h_slant_err);
+    h->h_slant_err = nullptr;
     (void)hipFree(h->d_min);
     (void)hipFree(h->d_zero);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -636,6 +640,7 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     sa.p2 = (float)h->p.p2;
     sa.uniq = h->p.uniqueness;
     sa.nviews = nv;
+    sa.err_host = h->d_slant_err;
 #ifdef SGM_SLANT_DEBUG
     if (getenv("SGM_SLANT_T56SWEEP")) {  // T56 by the two diagonal sweeps instead
         for (int v = 0; v < nv; ++v) {
@@ -1004,6 +1009,10 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             if (!rc) rc = dalloc(h, &h->d_gran, ng);
             if (!rc) rc = dalloc(h, &h->d_slant_ctl, 2);
             if (!rc) rc = dalloc(h, &h->d_slant_dummy, 512);
+            if (!rc && (hipHostMalloc((void **)&h->h_slant_err, sizeof(unsigned), hipHostMallocMapped) != hipSuccess ||
+                        hipHostGetDevicePointer((void **)&h->d_slant_err, h->h_slant_err, 0) != hipSuccess))
+                rc = set_err(h, SGM_ERR_HIP, "hipHostMalloc of the slanted schedule's hang-guard word failed");
+            if (!rc) *h->h_slant_err = 0;
             if (!rc && (hipMemset(h->d_gran, 0, ng * sizeof(unsigned long long)) != hipSuccess ||
                         hipMemset(h->d_slant_ctl, 0, 2 * sizeof(sgm::SlantCtl)) != hipSuccess))
                 rc = set_err(h, SGM_ERR_HIP, "hipMemset of the slanted schedule's hand-off state failed");
@@ -1071,10 +1080,21 @@ size_t sgm_device_bytes(const sgm_handle *h) { return h ? h->bytes : 0; }
 
 void *sgm_get_stream(const sgm_handle *h) { return h ? (void *)h->st : nullptr; }
 
+// The slanted passes' hang guard (sgm_slant.hip): a receiver that polls a
+// neighbouring tile's hand-off for seconds gives up, and that frame's maps
+// are wrong.  It sets a host-mapped word; the next call on the handle (or
+// sgm_process, after its own frame) reports it and clears it.
+int check_slant_err(sgm_handle *h) {
+    if (!h->h_slant_err || !*(volatile unsigned *)h->h_slant_err) return SGM_OK;
+    *(volatile unsigned *)h->h_slant_err = 0;
+    return set_err(h, SGM_ERR_HIP, "slanted aggregation: a tile hand-off timed out; that frame's maps are invalid");
+}
+
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
                        float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream) {
     if (!h) return SGM_ERR_INVALID_ARG;
+    if (int rc = check_slant_err(h)) return rc;
     if (!d_left || !d_right || !d_out || pitch < h->p.width || out_pitch < h->g.W ||
         ((d_sky_l || d_sky_r) && sky_pitch < h->g.W))
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process_device: bad pointer or pitch");
@@ -1096,9 +1116,10 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: bad pointer or pitch");
     if (h->p.aux_only)
         return set_err(h, SGM_ERR_INVALID_ARG, "sgm_process: handle created with aux_only");
+    int rc;
+    if ((rc = check_slant_err(h))) return rc;
     DeviceGuard guard(h->device);
     StreamScope scope(h, nullptr);
-    int rc;
     if ((rc = ensure_pinned(h))) return rc;
     const size_t nin = (size_t)h->p.height * h->p.width, npx = (size_t)h->g.H * h->g.W;
     uint8_t *pl = h->h_pin, *pr = pl + nin, *psl = pr + nin, *psr = psl + npx;
@@ -1125,6 +1146,7 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
         HIPCHK(h, hipMemcpyAsync(praw, h->d_disp[0], npx * sizeof(uint16_t), hipMemcpyDeviceToHost,
                                  h->st));
     HIPCHK(h, hipStreamSynchronize(h->st));
+    if ((rc = check_slant_err(h))) return rc;
     for (int i = 0; i < h->g.H; ++i)
         memcpy(out + (size_t)i * out_pitch, pout + (size_t)i * h->g.W, h->g.W * sizeof(float));
     if (raw_disp) memcpy(raw_disp, praw, npx * sizeof(uint16_t));

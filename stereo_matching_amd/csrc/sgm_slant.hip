@@ -284,7 +284,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #endif
                         if (__all(decode())) break;
                         if (spins >= kSlantSpinLimit) {
-                            if (lane == 0) atomicOr(&ctl->err, 1u);
+                            if (lane == 0) {
+                                atomicOr(&ctl->err, 1u);
+                                // (the host reports it: sgm_capi.hip check_slant_err)
+                                __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            }
                             break;
                         }
                     }

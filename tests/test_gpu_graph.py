@@ -15,9 +15,17 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.parametrize("h,w,D,views,sky", [(96, 320, 64, 2, False), (375, 1242, 128, 1, False),
-                                             (120, 256, 128, 2, True)])
-def test_frame_replays_from_a_hip_graph(h, w, D, views, sky):
+@pytest.mark.parametrize("h,w,D,views,sky,slant", [(96, 320, 64, 2, False, False),
+                                                   (375, 1242, 128, 1, False, False),
+                                                   (120, 256, 128, 2, True, False),
+                                                   # the slanted passes: their tickets and
+                                                   # granule tags live on the device and move
+                                                   # on every launch, replays included
+                                                   (96, 320, 64, 2, False, True),
+                                                   (120, 256, 256, 2, True, True),
+                                                   (80, 200, 128, 1, False, True)])
+def test_frame_replays_from_a_hip_graph(h, w, D, views, sky, slant, monkeypatch):
+    monkeypatch.setenv("SGM_SLANT", "1" if slant else "0")
     dev = torch.device("cuda", 0)
     with SGM(h, w, 1, D, views=views) as sgm:
         stream = torch.cuda.ExternalStream(sgm.stream, device=dev)

@@ -126,3 +126,21 @@ def test_calls_on_different_streams_are_ordered():
     r = subprocess.run([sys.executable, "-c", CROSS_STREAM, root], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "cross-stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("views,slanted", [(2, True), (1, False)])
+def test_slant_default_by_size(views, slanted, monkeypatch):
+    # sgm_capi.hip slant_default: at D = 256 above the Infinity Cache the
+    # slanted passes run once every workgroup gets a full-height tile of work
+    # (HD256 two views: views x W = 3840 >= 14 x 256 CUs), else the bands
+    monkeypatch.delenv("SGM_SLANT", raising=False)
+    h, w, D = 1080, 1920, 256
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=0)
+    with SGM(h, w, 1, D, views=views) as sgm:
+        sgm.set_profiling(True)
+        sgm.process(left, right)
+        prof = sgm.get_profile()
+    assert ("slant_up" in prof) == slanted, sorted(prof)
+    assert ("stage_a_d" in prof) == (not slanted), sorted(prof)
+
