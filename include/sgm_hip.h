@@ -170,7 +170,13 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
 /* Same on DEVICE buffers, enqueued on `stream` (a hipStream_t; NULL = the
  * handle's own stream).  Returns after enqueueing; the caller synchronises.
  * With params.post_filter the call synchronises `stream` during the median
- * fill's convergence test (sgm_post_filter_device). */
+ * fill's convergence test (sgm_post_filter_device).
+ * Volumes above the Infinity Cache may run the slanted-tile passes
+ * (DESIGN.md 5e), whose tile-to-tile hand-offs poll with a bounded spin: a
+ * frame in which a poll gave up (seconds without progress: a hung or
+ * preempted neighbour) has invalid maps, and the NEXT sgm_process_device /
+ * sgm_process call on the handle returns SGM_ERR_HIP for it (sgm_process
+ * also checks right after its own frame). */
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
                        float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream);
