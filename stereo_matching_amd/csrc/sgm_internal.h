@@ -158,6 +158,7 @@ struct SlantArgs {
     float p1, p2, uniq;
     int nviews;
     int ntiles, grid;   // set by the launcher
+    int max_grid;       // workgroups at most (0: one per CU)
     unsigned *err_host; // host-mapped word set to 1 when a hand-off poll gives up
 };
 size_t slant_tiles(Geom g);

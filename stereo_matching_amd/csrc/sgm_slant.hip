@@ -568,6 +568,7 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
         cus = 256;
     const int total = a.ntiles * a.nviews;
     a.grid = total < cus ? total : cus;
+    if (a.max_grid > 0 && a.max_grid < a.grid) a.grid = a.max_grid;
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_GRID")) a.grid = atoi(e) > 0 && atoi(e) < a.grid ? atoi(e) : a.grid;
 #endif
