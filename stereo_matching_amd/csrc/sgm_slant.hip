@@ -226,9 +226,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             auto gstep = [&](int p) { return uniform(gvalid(p) ? s_begin - 1 + p : s_begin); };
             unsigned long long rq[CR][NX][V];
             auto issue = [&](int slot, int p) {
-#ifdef SLANT_PROBE_NOCOURIER
-                return;  // timing probe: no hand-off loads (wrong results)
-#endif
                 const int ss = gstep(p);
 #pragma unroll
                 for (int x = 0; x < NX; ++x) load_granules<V>(rq[slot][x], rrs, (ss * 3 + x) * D * 8 + goff);
@@ -262,9 +259,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                             y[x][v] = granule_value(q);
                             ok &= (unsigned)!need[x] | granule_ok(q, tag);
                         }
-#if defined(SLANT_PROBE_NOWAIT) || defined(SLANT_PROBE_NOCOURIER)
-                    ok = 1u;  // timing probe: no hand-off wait (wrong results)
-#endif
                     return (ok | (unsigned)!dact) != 0u;
                 };
                 if (!__all(decode())) {
@@ -363,13 +357,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         const bool never = s_lo > s_hi;
         auto off_of = [&](int s) -> long long {
             const int sc = uniform(min(max(s, s_lo), s_hi));
-#ifdef SLANT_PROBE_HOT
-            // timing probe: every stream load from one small L2-resident
-            // block, every store to the dummy area (wrong results)
-            return (long long)sc * 0 + (long long)(k * 64 * V + e0) + (never ? 0 : 0);
-#else
             return never ? (long long)e0 : base + (long long)sc * dstep;
-#endif
         };
         constexpr int NS = UP ? 4 : 1;  // streams: C (+ S12, L3, T56)
         float rb[NS][PF][V];
@@ -378,15 +366,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             const long long o = off_of(pfs);
             load_v<V>(rb[0][slot], sv.cost + o, dact);
             if constexpr (UP) {
-#ifndef SLANT_PROBE_NOLOADS
                 load_v_nt<V>(rb[1][slot], sv.s12 + o, dact);
                 load_v_nt<V>(rb[2][slot], sv.l3 + o, dact);
                 load_v_nt<V>(rb[3][slot], sv.t56 + o, dact);
-#else
-                load_v<V>(rb[1][slot], sv.cost + o, dact);
-                load_v<V>(rb[2][slot], sv.cost + o, dact);
-                load_v<V>(rb[3][slot], sv.cost + o, dact);
-#endif
             }
             ++pfs;
         };
@@ -407,12 +389,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         auto wta_out = [&](const float (&tt)[V], int ps) {
             int d;
             float f;
-#ifdef SLANT_PROBE_NOWTA
-            d = 0;  // timing probe: no WTA (wrong results)
-            f = tt[0];
-#else
             wta_subpixel<V>(tt, D, a.uniq, d, f);
-#endif
             // outputs: an inactive step writes the dummy words instead
             const int j = u + ps;
             const bool act = ps >= 0 && j >= 0 && j < W;
@@ -478,25 +455,17 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     tot[v] = ((rb[1][q][v] + rb[2][q][v]) + L4[v]) + ((rb[3][q][v] + Lo[v]) + L2[v]);
                 store_lds_v<V>(&L.st[cp][k][0][e0], L4);
                 if (lane == 0) L.pm[cp][k][0] = n4;
-#ifdef SLANT_WTA_INLINE
-                wta_out(tot, s);
-#else
                 wta_out(ptot, pstep);
 #pragma unroll
                 for (int v = 0; v < V; ++v) ptot[v] = tot[v];
                 pstep = s;
-#endif
             } else {
                 store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, L2, tag);
                 // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
                 float o[V];
 #pragma unroll
                 for (int v = 0; v < V; ++v) o[v] = Lo[v] + L2[v];
-#ifdef SLANT_PROBE_HOT
-                float *dst = a.dummy + e0;
-#else
                 float *dst = act ? sv.t56w + off_of(s) : a.dummy + e0;
-#endif
                 store_v_nt<V>(dst, o, dact);
             }
             store_lds_v<V>(&L.st[cp][k][K2][e0], L2);
@@ -523,9 +492,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
         for (int q = 0; q < PF; ++q)
             if (s0 + q < s_end) step(q, s0 + q);
-#ifndef SLANT_WTA_INLINE
         if constexpr (UP) wta_out(ptot, pstep);
-#endif
 #ifdef SGM_SLANT_STAMPS
         if (k == 0 && lane == 0) {
             SLANT_STAMP(0, nsteps);
