@@ -674,14 +674,22 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     // chains; the tile-to-tile hand-off chain), so together they fill the
     // memory system better than one after the other: HD256 13.44 -> 12.72,
     // 4K256 48.03 -> 46.31 ms per frame (profiles/r04_experiments/slant.txt).
-    HIPCHK(h, hipEventRecord(h->ev_fork, st));
-    HIPCHK(h, hipStreamWaitEvent(h->st_h, h->ev_fork, 0));
+    // (profiled as one more entry, "slant_down_hpair": fork to join on the
+    // frame's stream, the pair's wall time; the two launches' own entries
+    // overlap in time)
     sa.max_grid = kSlantDownGridNum * slant_cus() / kSlantDownGridDen;
-    HIPCHK(h, timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); }));
-    HIPCHK(h, timed(h, "stage_a_h", nv * elems, h->st_h,
-                    [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, h->st_h); }));
-    HIPCHK(h, hipEventRecord(h->ev_join, h->st_h));
-    HIPCHK(h, hipStreamWaitEvent(st, h->ev_join, 0));
+    HIPCHK(h, timed(h, "slant_down_hpair", nv * elems, st, [&] {
+        hipError_t e = hipEventRecord(h->ev_fork, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->st_h, h->ev_fork, 0);
+        if (e == hipSuccess)
+            e = timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); });
+        if (e == hipSuccess)
+            e = timed(h, "stage_a_h", nv * elems, h->st_h,
+                      [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, h->st_h); });
+        if (e == hipSuccess) e = hipEventRecord(h->ev_join, h->st_h);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, h->ev_join, 0);
+        return e;
+    }));
     sa.max_grid = 0;
     HIPCHK(h, timed(h, "slant_up", nv * elems, st, [&] { return sgm::launch_slant_up(sa, g, st); }));
     return SGM_OK;

@@ -3,3 +3,4 @@ timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thre
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r04f_smoke.log 2>&1; tail -1 gpurun_out/r04f_smoke.log
 GIT_SHA=$1 bash tools/round.sh r04f bench prof pmc || exit 1
 cp profiles/pmc_traffic.json gpurun_out/r04f_pmc_traffic_all.json
+for c in hd256 4k256 4k256full; do echo "$c: $(python tools/trace_span.py gpurun_out/r04f_prof_$c/run_kernel_trace.csv | head -1)"; done
