@@ -334,12 +334,13 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
 
 // The slanted-tile schedule replaces the bands (above the Infinity Cache)
 // where it was measured faster (tools/slant_sizes.py,
-// profiles/r04_experiments/slant.txt): at D = 256 once every workgroup gets a
-// full-height tile's worth of steps, views * W * H / (NW * CUs) >= H (HD256
-// two views -13.9%, 4K256 one view -14.2%, two views -19%; HD256 one view
-// +12.9%, 720p D = 256 two views +3.0%); at D = 128 from two tiles per
-// workgroup (4K128 two views -4.9%; HD128 -2.4%); never at D = 64 (HD64 two
-// views +19.5%).  Below those sizes the tile-to-tile hand-off chain, not the
+// profiles/r04_experiments/slant.txt, with the H pair beside the top-down
+// pass): at D >= 128 once views * W >= 0.7 * NW * CUs, i.e. 0.7 full-height
+// tiles of work per workgroup (HD256 two views -18.6%, 4K256 one view -20%,
+// two views -24%, 720p D = 256 two views -9.4%, HD128 two views -9.6%,
+// 4K128 two views -18.8%; HD256 one view +2.0%, HD128 one view +24.9%,
+// 1056x512 D = 128 two views +10.3%); never at D = 64 (HD64 two views
+// +16.8%, 4K64 +4.2%).  Below that the tile-to-tile hand-off chain, not the
 // bytes, sets the passes' time.
 bool slant_default(Geom g, int nviews) {
     const double vol = (double)g.W * g.H * g.D * sizeof(float);
@@ -348,8 +349,7 @@ bool slant_default(Geom g, int nviews) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const long long tiles_per_wg = g.D >= 256 ? 1 : 2;
-    return (long long)nviews * g.W >= tiles_per_wg * sgm::kSlantNW * cus;
+    return 10LL * nviews * g.W >= 7LL * sgm::kSlantNW * cus;
 }
 
 // Rows per band of the backward phase (stage B's diagonal pair, the L8
@@ -617,8 +617,10 @@ int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, i
 //   H pair (both views): S12 = L1 + L2
 //   slant_up (both views): L4, L7, L8 walking up, total
 //     ((S12 + L3) + L4) + ((T56 + L7) + L8), WTA, sub-pixel (row-major maps)
-// the top-down pass's share of the CUs while the H pair runs beside it
-constexpr int kSlantDownGridNum = 1, kSlantDownGridDen = 2;
+// the top-down pass's share of the CUs (eighths) while the H pair runs
+// beside it: measured best at 4/8 for D = 256 and 6/8 for D = 128 (HD256,
+// 4K256 one and two views, 4K128: profiles/r04_experiments/slant.txt)
+int slant_down_grid_eighths(int D) { return D >= 256 ? 4 : 6; }
 int slant_cus() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -677,7 +679,7 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     // (profiled as one more entry, "slant_down_hpair": fork to join on the
     // frame's stream, the pair's wall time; the two launches' own entries
     // overlap in time)
-    sa.max_grid = kSlantDownGridNum * slant_cus() / kSlantDownGridDen;
+    sa.max_grid = slant_down_grid_eighths(g.D) * slant_cus() / 8;
     HIPCHK(h, timed(h, "slant_down_hpair", nv * elems, st, [&] {
         hipError_t e = hipEventRecord(h->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->st_h, h->ev_fork, 0);

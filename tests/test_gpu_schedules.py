@@ -131,9 +131,10 @@ def test_calls_on_different_streams_are_ordered():
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("views,slanted", [(2, True), (1, False)])
 def test_slant_default_by_size(views, slanted, monkeypatch):
-    # sgm_capi.hip slant_default: at D = 256 above the Infinity Cache the
-    # slanted passes run once every workgroup gets a full-height tile of work
-    # (HD256 two views: views x W = 3840 >= 14 x 256 CUs), else the bands
+    # sgm_capi.hip slant_default: at D >= 128 above the Infinity Cache the
+    # slanted passes run once every workgroup gets 0.7 full-height tiles of
+    # work (HD256 two views: views x W = 3840 >= 0.7 x 14 x 256 CUs; one
+    # view, 1920, below it), else the bands
     monkeypatch.delenv("SGM_SLANT", raising=False)
     h, w, D = 1080, 1920, 256
     left, right = synthetic.stereo_pair(h, w, D, pair_index=0)
