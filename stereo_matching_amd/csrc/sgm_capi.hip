@@ -635,11 +635,18 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     const double elems = (double)g.H * g.W * g.D;
     sgm::PairArgs hp1[2], hp2[2];
     sgm::SlantArgs sa{};
-    for (int v = 0; v < nv; ++v) {
+    if (nv == 2) {  // both views in one launch
+        const sgm::PairArgs pa[2] = {pair_args(h), pair_args(h)};
+        const float *in[2] = {h->d_ch[0], h->d_ch[1]};
+        float *out[2] = {h->d_c[0], h->d_c[1]}, *l3[2] = {h->d_l3[0], h->d_l3[1]};
+        HIPCHK(h, timed(h, "vfwd_l3", 2 * elems, st, [&] { return sgm::launch_vfwd2_l3(in, out, l3, pa, g, st); }));
+    } else {
         const sgm::PairArgs pa = pair_args(h);
         HIPCHK(h, timed(h, "vfwd_l3", elems, st, [&] {
-                   return sgm::launch_vfwd_l3(h->d_ch[v], h->d_c[v], h->d_l3[v], pa, g, st);
+                   return sgm::launch_vfwd_l3(h->d_ch[0], h->d_c[0], h->d_l3[0], pa, g, st);
                }));
+    }
+    for (int v = 0; v < nv; ++v) {
         hp1[v] = pair_args(h);
         hp1[v].cost = h->d_c[v];
         hp1[v].ckpt = h->d_ck[v][sgm::PAIR_H];

@@ -40,6 +40,18 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     vfwd_body<V, FULL, WIN, PF, BAND, L3OUT>(in, out, a, g, bid_x(), tid_x());
 }
 
+// Both views' vertical passes writing C and the whole L3 volume (the slanted
+// schedule) in one launch, workgroup y = view: W chains per view leave about
+// two waves per SIMD at HD, one launch of 2W about four.
+template <int V, bool FULL, int WIN, int PF>
+__global__ __launch_bounds__(64) void vfwd2_l3_kernel(const float *__restrict__ in0, float *__restrict__ out0,
+                                                      PairArgs a0, const float *__restrict__ in1,
+                                                      float *__restrict__ out1, PairArgs a1, Geom g) {
+    const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
+    vfwd_body<V, FULL, WIN, PF, false, true>(vb ? in1 : in0, vb ? out1 : out0, vb ? a1 : a0, g, bid_x(),
+                                             tid_x());
+}
+
 template <int FD, int V, bool FULL, int PF>
 __global__ __launch_bounds__(64) void pair_fwd_kernel(PairArgs a, Geom g) {
     pair_fwd_body<FD, V, FULL, PF>(a, g, bid_x());
@@ -310,6 +322,26 @@ hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs
     b.out = l3;
     if (g.scale == 1) launch_vfwd_t<3, false, true>(in, out, b, g, st);
     else launch_vfwd_t<1, false, true>(in, out, b, g, st);
+    return hipGetLastError();
+}
+
+template <int WIN>
+static void launch_vfwd2_l3_t(const float *const *in, float *const *out, const PairArgs *b, Geom g,
+                              hipStream_t st) {
+    const dim3 grid(g.W, 2);
+    if (g.D == 32) vfwd2_l3_kernel<1, false, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+    else if (g.D == 64) vfwd2_l3_kernel<1, true, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+    else if (g.D == 128) vfwd2_l3_kernel<2, true, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+    else vfwd2_l3_kernel<4, true, WIN, 8><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+}
+
+hipError_t launch_vfwd2_l3(const float *const *in, float *const *out, float *const *l3, const PairArgs *a,
+                           Geom g, hipStream_t st) {
+    PairArgs b[2] = {a[0], a[1]};
+    b[0].out = l3[0];
+    b[1].out = l3[1];
+    if (g.scale == 1) launch_vfwd2_l3_t<3>(in, out, b, g, st);
+    else launch_vfwd2_l3_t<1>(in, out, b, g, st);
     return hipGetLastError();
 }
 

@@ -48,6 +48,8 @@ def short(name):
     # the slanted passes, and vfwd writing the whole L3 volume (template L3OUT)
     if "slant_kernel<" in name:
         return "slant_up" if name.split("slant_kernel<")[1].startswith("true") else "slant_down"
+    if "vfwd2_l3_kernel" in name:
+        return "vfwd_l3"
     if "vfwd_kernel<" in name:
         args = name[name.index("vfwd_kernel<") + len("vfwd_kernel<"):].split(">")[0].split(", ")
         if len(args) >= 6 and args[5] == "true":
