@@ -17,7 +17,7 @@ bad = 0
 for it in range(n):
     D = int(rng.choice([32, 64, 128, 256]))
     h = int(rng.integers(3, 260))
-    w = int(rng.integers(3, 700))
+    w = int(rng.integers(5, 700))  # (the 5x3 cost window: sgm_create rejects W < 5)
     views = int(rng.integers(1, 3))
     maps = {}
     for m in ("0", "1"):
