@@ -219,8 +219,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        # a SCALE line must describe the ranks that ran: refuse a mismatch
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world} (launch N ranks "
+                         f"with --gpus N)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # under torch.distributed.run (the driver's launch line for N > 1, and the
@@ -247,6 +249,7 @@ def main():
         from stereo_matching_amd.distributed import PipelinedGather
         pipe = PipelinedGather((gk, h, w) if gk > 1 else (h, w), torch.float32, dev, depth=2)
     nstep = [0]
+    verified = []
 
     if cfg.get("full"):
         args.post_filter = args.lk_refine = args.sky_detect = True
@@ -268,6 +271,32 @@ def main():
     stream = (torch.cuda.Stream(dev) if args.caller_stream
               else torch.cuda.ExternalStream(sgm.stream, device=dev))
     torch.cuda.set_stream(stream)
+    if pipe:
+        pipe.check = sgm.check
+
+    def verify(what):
+        """After a pass: sgm_check on every rank (waits for the frames; raises
+        if a slanted-pass hand-off gave up in one), agreed across ranks, so
+        no invalid frame is timed or gathered as valid; exits non-zero."""
+        try:
+            if pipe:
+                pipe.verify()
+            else:
+                err = None
+                try:
+                    sgm.check()
+                except Exception as e:  # noqa: BLE001 -- agreed on below
+                    err = e
+                if distributed:
+                    from stereo_matching_amd.distributed import agree
+                    if not agree(err is None) and err is None:
+                        err = RuntimeError("a frame on another rank is invalid")
+                if err is not None:
+                    raise err
+        except Exception as e:  # noqa: BLE001
+            print(f"bench.py: the {what} pass produced invalid frames: {e}", file=sys.stderr)
+            sys.exit(3)
+        verified.append(what)
 
     def step():
         if team:
@@ -292,8 +321,9 @@ def main():
         step()
     flush()
     if pipe:
-        pipe.drain()
+        pipe.drain(verify=False)
     torch.cuda.synchronize(dev)
+    verify("warmup")
     eager_step = step
     if args.graph:
         # the frame's launches recorded once on the handle's stream (no event
@@ -323,17 +353,22 @@ def main():
             step()
         flush()
         if pipe:
-            pipe.drain()  # every gather of the timed steps is inside the timed region
+            pipe.drain(verify=False)  # every gather of the timed steps is inside the timed region
         torch.cuda.synchronize(dev)
         if distributed:
             dist.barrier()
         return time.perf_counter() - t0
 
     elapsed = timed_steps(args.steps)
+    verify("timed")
+    rank_min = rank_max = elapsed
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        rank_max = elapsed = float(t.item())
+        t = torch.tensor([rank_min], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        rank_min = float(t.item())
 
     pairs = world // 2 if args.view_split else world
     units = float(pairs) * views * h * w * D * args.steps
@@ -347,6 +382,7 @@ def main():
         sgm.set_profiling(True)
         step = eager_step
         prof_elapsed = timed_steps(args.steps)
+        verify("profile")
         prof = sgm.get_profile()
         sgm.set_profiling(False)
         for name, (n, total_ms, elems) in prof.items():
@@ -561,6 +597,13 @@ def main():
                                            else "overlapped with the next step")) if distributed else
                                        "1 pair on 1 GPU (single process: no process group, no "
                                        "gather)")},
+            # what the process group saw (the driver's SCALE runs check it
+            # against n_gpus), and the spread of the timed region over ranks
+            "backend": dist.get_backend() if distributed else None,
+            "world_size_seen": dist.get_world_size() if distributed else 1,
+            "rank_timed_s": {"min": round(rank_min, 6), "max": round(rank_max, 6)},
+            # passes whose frames sgm_check found valid on every rank
+            "frames_verified": verified,
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
             **({"cpu_baseline_note": cpu_note} if cpu_note else {}),
             "host_io": host_io,

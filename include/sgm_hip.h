@@ -174,12 +174,25 @@ int sgm_process(sgm_handle *h, const uint8_t *left, const uint8_t *right, int pi
  * Volumes above the Infinity Cache may run the slanted-tile passes
  * (DESIGN.md 5e), whose tile-to-tile hand-offs poll with a bounded spin: a
  * frame in which a poll gave up (seconds without progress: a hung or
- * preempted neighbour) has invalid maps, and the NEXT sgm_process_device /
- * sgm_process call on the handle returns SGM_ERR_HIP for it (sgm_process
- * also checks right after its own frame). */
+ * preempted neighbour; later polls of that launch then skip their wait) has
+ * invalid maps.  sgm_check() reports it once the frame's work is done; the
+ * NEXT sgm_process_device / sgm_process call on the handle also returns
+ * SGM_ERR_HIP for it (sgm_process checks right after its own frame). */
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
                        float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream);
+
+/* Post-sync validity check of the frames enqueued so far (the reference has
+ * no asynchronous work to check: SGM::process is synchronous, SGM.cpp:32-826).
+ * Waits for the handle's last call's work (its stream, or the event the call
+ * recorded on the caller's stream), then returns SGM_ERR_HIP, with the
+ * message in sgm_last_error, if any slanted-pass hand-off gave up since the
+ * last report -- the maps of the frames in between are then invalid -- and
+ * clears the report; else SGM_OK.  Frames replayed from a captured HIP graph
+ * are not calls on the handle: synchronise the graph's stream first, then
+ * call sgm_check.  A caller that gathers or times maps should call it after
+ * synchronising and before trusting them. */
+int sgm_check(sgm_handle *h);
 
 /* The LR check of SGM.cpp:803-818 on DEVICE working-grid maps: out(i, j) =
  * fl(i, j), or D+1 where j >= fl and |fl - fr(i, (int)(j - fl/s))| > lr_max_diff.
@@ -240,6 +253,54 @@ int sgm_colormap_device(sgm_handle *h, const float *d_disp, int pitch, uint8_t *
 int sgm_point_cloud_device(sgm_handle *h, const float *d_disp, int pitch, const uint8_t *d_img,
                            int img_pitch, const sgm_camera *cam, double *d_xyz,
                            uint8_t *d_pixel, int *d_count, void *stream);
+
+/* ---- multi-GPU: pairs shard one per device, maps gathered to rank 0 ----
+ *
+ * stereo pairs are independent, so a batch runs one pair per
+ * GPU (one sgm_handle per device) and the only collective is the gather of
+ * the H x W disparity maps to rank 0: RCCL's ncclGather over xGMI (1.86 MB
+ * per rank at K128).  The reference has no multi-GPU path; its per-pair call
+ * is node.cpp:49,93 (SGM sgm(h, w, s, d); sgm.process(l, r)), which
+ * include/sgm_amd/BatchSGM.h runs on every device of a batch, one host
+ * thread per device.  RCCL is bound at run time on the first sgm_comm_*
+ * call (an RCCL the process already holds, e.g. PyTorch's, is reused;
+ * SGM_RCCL_LIB names another).  Errors before a communicator exists are
+ * read with sgm_comm_last_error(NULL). */
+typedef struct sgm_comm sgm_comm;
+
+#define SGM_COMM_ID_BYTES 128  /* = sizeof(ncclUniqueId) */
+
+/* Single process driving n devices, ranks 0..n-1 = devices[0..n-1]
+ * (ncclCommInitAll).  Each device appears once. */
+int sgm_comm_create(const int *devices, int n, sgm_comm **out);
+/* One process per device (the torch.distributed.run layout): rank 0 makes an
+ * id, every process receives it out of band and joins as `rank` of `nranks`
+ * on `device` (ncclGetUniqueId / ncclCommInitRank; blocks until all joined). */
+int sgm_comm_unique_id(char id[SGM_COMM_ID_BYTES]);
+int sgm_comm_create_rank(const char id[SGM_COMM_ID_BYTES], int nranks, int rank, int device,
+                         sgm_comm **out);
+int sgm_comm_destroy(sgm_comm *c);
+const char *sgm_comm_last_error(const sgm_comm *c);
+/* ranks in the communicator, the first rank this object holds, and how many */
+int sgm_comm_info(const sgm_comm *c, int *nranks, int *first_rank, int *nlocal);
+
+/* Rank `rank`'s contribution to the gather (ncclGather, root 0): its DEVICE
+ * map d_map (rows x cols f32, row pitch in floats >= cols; pitched maps are
+ * packed first) lands at d_root_out + rank * rows * cols on rank 0's device
+ * (nranks * rows * cols floats; ignored on other ranks).  Enqueued on
+ * `stream`, a hipStream_t of the rank's device (NULL: the legacy default
+ * stream), after the map's producer on that stream; returns after
+ * enqueueing.  Every rank of the communicator must call it with the same
+ * rows and cols: from its own host thread, or through sgm_batch_gather_all
+ * when one thread drives all ranks.  Call sgm_check on the producing handle
+ * first: a map from a frame sgm_check rejects is not valid. */
+int sgm_batch_gather(sgm_comm *c, int rank, const float *d_map, int rows, int cols, int pitch,
+                     float *d_root_out, void *stream);
+/* The same for every rank this object holds, from one thread (one RCCL
+ * group): d_maps[k] and streams[k] (NULL array: default streams) belong to
+ * rank first_rank + k. */
+int sgm_batch_gather_all(sgm_comm *c, const float *const *d_maps, int rows, int cols, int pitch,
+                         float *d_root_out, void *const *streams);
 
 /* ---- per-kernel timing (HIP events recorded around every launch) ---- */
 

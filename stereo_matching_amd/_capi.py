@@ -33,8 +33,11 @@ EXPORTS = (
     "sgm_stage_aggregate", "sgm_stage_lr", "sgm_stage_post_filter", "sgm_set_profiling",
     "sgm_get_profile", "sgm_lk_refine_device", "sgm_stage_lk_refine", "sgm_sky_detect_device",
     "sgm_stage_sky_detect", "sgm_colormap_device", "sgm_point_cloud_device", "sgm_stage_colormap",
-    "sgm_stage_point_cloud", "sgm_lr_check_device", "sgm_get_stream",
+    "sgm_stage_point_cloud", "sgm_lr_check_device", "sgm_get_stream", "sgm_check",
+    "sgm_comm_create", "sgm_comm_unique_id", "sgm_comm_create_rank", "sgm_comm_destroy",
+    "sgm_comm_last_error", "sgm_comm_info", "sgm_batch_gather", "sgm_batch_gather_all",
 )
+SGM_COMM_ID_BYTES = 128
 
 
 class SGMError(RuntimeError):
@@ -102,6 +105,7 @@ def lib():
     L.sgm_get_stream.restype = ctypes.c_void_p
     L.sgm_process.argtypes = [P, P, P, I, P, P, I, P, I, P]
     L.sgm_process_device.argtypes = [P, P, P, I, P, P, I, P, I, P, P]
+    L.sgm_check.argtypes = [P]
     L.sgm_post_filter_device.argtypes = [P, P, I, P]
     L.sgm_lr_check_device.argtypes = [P, P, I, P, I, P, I, P]
     L.sgm_stage_post_filter.argtypes = [P, P]
@@ -121,8 +125,17 @@ def lib():
     L.sgm_stage_lr.argtypes = [P, P, P, P]
     L.sgm_set_profiling.argtypes = [P, I]
     L.sgm_get_profile.argtypes = [P, ctypes.POINTER(KernelStat), I, ctypes.POINTER(I)]
+    L.sgm_comm_create.argtypes = [ctypes.POINTER(I), I, ctypes.POINTER(P)]
+    L.sgm_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.sgm_comm_create_rank.argtypes = [ctypes.c_char_p, I, I, I, ctypes.POINTER(P)]
+    L.sgm_comm_destroy.argtypes = [P]
+    L.sgm_comm_last_error.argtypes = [P]
+    L.sgm_comm_last_error.restype = ctypes.c_char_p
+    L.sgm_comm_info.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)]
+    L.sgm_batch_gather.argtypes = [P, I, P, I, I, I, P, P]
+    L.sgm_batch_gather_all.argtypes = [P, ctypes.POINTER(P), I, I, I, P, ctypes.POINTER(P)]
     for name in EXPORTS:
-        if name not in ("sgm_last_error", "sgm_device_bytes", "sgm_get_stream"):
+        if name not in ("sgm_last_error", "sgm_device_bytes", "sgm_get_stream", "sgm_comm_last_error"):
             getattr(L, name).restype = I
     _lib = L
     return L

@@ -1137,6 +1137,17 @@ int check_slant_err(sgm_handle *h) {
     return set_err(h, SGM_ERR_HIP, "slanted aggregation: a tile hand-off timed out; that frame's maps are invalid");
 }
 
+int sgm_check(sgm_handle *h) {
+    if (!h) return SGM_ERR_INVALID_ARG;
+    DeviceGuard guard(h->device);
+    // the last call's work: on a caller's stream its end was recorded in
+    // ev_last; on the handle's own stream, that stream (the H pair's stream
+    // is joined into the frame's stream before the bottom-up pass)
+    if (h->last_st && h->last_recorded) HIPCHK(h, hipEventSynchronize(h->ev_last));
+    else HIPCHK(h, hipStreamSynchronize(h->st));
+    return check_slant_err(h);
+}
+
 int sgm_process_device(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int pitch,
                        const uint8_t *d_sky_l, const uint8_t *d_sky_r, int sky_pitch,
                        float *d_out, int out_pitch, uint16_t *d_raw_disp, void *stream) {

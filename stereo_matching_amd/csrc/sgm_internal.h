@@ -136,15 +136,20 @@ hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs
                           hipStream_t st);
 
 // ----------------------------------------------- slanted tiles (sgm_slant.hip)
-// Compute waves per tile (two more waves per workgroup carry the hand-offs:
-// one publishes the tile's exit states, one receives the next tile's).
+// Compute waves per tile; one more wave per workgroup, the receiver, turns
+// the next tile's exit-state granules into LDS states (the compute waves 0
+// and 1 store this tile's own exit states themselves).
 constexpr int kSlantNW = 14;
+// Polls before a receiver gives up on a hand-off (a hang guard: seconds).
+constexpr unsigned kSlantSpinLimit = 1u << 22;
 // Launch bookkeeping of one slanted pass kind, in device memory (zeroed at
 // create): tickets claim tiles, the last workgroup out resets tickets/exits
 // and advances epoch (the hand-off granules' tag), err counts hang-guard
-// give-ups.
+// give-ups, dead = epoch + 1 of the last launch in which a receiver gave up
+// (every later poll of that launch skips its wait, so one dead neighbour
+// costs one spin limit, not one per step).
 struct SlantCtl {
-    unsigned tickets, exits, epoch, err;
+    unsigned tickets, exits, epoch, err, dead;
 };
 struct SlantView {
     const float *cost, *s12, *l3, *t56;  // HWD: C, L1+L2, L3, L5+L6 (bottom-up reads)
@@ -163,6 +168,11 @@ struct SlantArgs {
     int ntiles, grid;   // set by the launcher
     int max_grid;       // workgroups at most (0: one per CU)
     unsigned *err_host; // host-mapped word set to 1 when a hand-off poll gives up
+    unsigned spin_limit;  // polls before giving up (kSlantSpinLimit; SGM_SLANT_DEBUG:
+                          // SGM_SLANT_SPIN_LIMIT)
+    int stall_tile;       // SGM_SLANT_DEBUG only (SGM_SLANT_STALL): the bottom-up pass's
+                          // receiver of this tile of view 0 never accepts a granule, to
+                          // exercise the give-up path; -1: none
 };
 size_t slant_tiles(Geom g);
 // granules (8 B each) of nviews views' hand-offs

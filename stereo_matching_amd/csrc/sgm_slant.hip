@@ -142,9 +142,6 @@ static __device__ unsigned long long slant_stamps[32];
 #define SLANT_STAMP(i, v) atomicAdd(&slant_stamps[(UP ? 16 : 0) + (i)], (unsigned long long)(v))
 #endif
 
-// polls before the receiver gives up (a hang guard: ~seconds; SlantCtl::err is set)
-constexpr unsigned kSlantSpinLimit = 1u << 22;
-
 // Exit states of a tile per step, as (wave, exchanged-state index) pairs:
 // bottom-up (w0 L4, w0 L8, w1 L8), top-down (w0 L6, w1 L6).
 template <bool UP>
@@ -189,6 +186,12 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
     if (tid_x() == 0)
         L.epoch = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float p2v = to_vgpr(a.p2);
+    // hang guard (receiver wave): once a poll of this launch gave up -- this
+    // wave's, or any workgroup's (ctl->dead == this launch's id) -- later
+    // polls skip their wait, so a neighbour that never stores costs one spin
+    // limit per launch, not one per step (the frame's maps are invalid
+    // anyway, and the host reports it: sgm_capi.hip check_slant_err)
+    unsigned dead = 0;
 
     for (;;) {
         __syncthreads();
@@ -207,6 +210,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         const int s_begin = max(0, -(u_lo + NW - 1));
         const int s_end = min(H, W - u_lo);
         const int nsteps = s_end - s_begin;
+#ifdef SGM_SLANT_DEBUG
+        const unsigned stall = (unsigned)(UP && view == 0 && t == a.stall_tile);
+#endif
 
         if (wave == NW) {
             // ----------------------------------------------- receiver wave
@@ -259,6 +265,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                             y[x][v] = granule_value(q);
                             ok &= (unsigned)!need[x] | granule_ok(q, tag);
                         }
+#ifdef SGM_SLANT_DEBUG
+                    ok &= stall ^ 1u;
+#endif
                     return (ok | (unsigned)!dact) != 0u;
                 };
                 if (!__all(decode())) {
@@ -267,7 +276,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     const long long sp0 = __builtin_amdgcn_s_memtime();
                     unsigned nsp = 0;
 #endif
-                    for (unsigned spins = 1;; ++spins) {
+                    const unsigned id = __builtin_amdgcn_readfirstlane(L.epoch) + 1u;
+                    const unsigned launch_id = id ? id : 1u;
+                    dead |= (unsigned)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                           &ctl->dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == launch_id);
+                    for (unsigned spins = 1; !dead; ++spins) {
                         __builtin_amdgcn_s_sleep(1);
                         // (a compiler barrier: the re-poll loads stay inside the loop)
                         asm volatile("" ::: "memory");
@@ -277,13 +290,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                         nsp = spins;
 #endif
                         if (__all(decode())) break;
-                        if (spins >= kSlantSpinLimit) {
+                        if (spins >= a.spin_limit) {
                             if (lane == 0) {
-                                atomicOr(&ctl->err, 1u);
+                                atomicAdd(&ctl->err, 1u);
+                                atomicExch(&ctl->dead, launch_id);
                                 // (the host reports it: sgm_capi.hip check_slant_err)
                                 __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                             }
-                            break;
+                            dead = 1u;
                         }
                     }
 #ifdef SGM_SLANT_STAMPS
@@ -536,8 +550,12 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
     const int total = a.ntiles * a.nviews;
     a.grid = total < cus ? total : cus;
     if (a.max_grid > 0 && a.max_grid < a.grid) a.grid = a.max_grid;
+    a.spin_limit = kSlantSpinLimit;
+    a.stall_tile = -1;
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_GRID")) a.grid = atoi(e) > 0 && atoi(e) < a.grid ? atoi(e) : a.grid;
+    if (const char *e = getenv("SGM_SLANT_SPIN_LIMIT")) a.spin_limit = atoi(e) > 0 ? (unsigned)atoi(e) : a.spin_limit;
+    if (const char *e = getenv("SGM_SLANT_STALL")) a.stall_tile = *e ? atoi(e) : -1;
 #endif
     const dim3 grid(a.grid), block(64 * (kSlantNW + 1));
 #ifndef SLANT_PF_UP4

@@ -59,8 +59,17 @@ def comm_device(group=None) -> torch.device:
     return torch.device("cpu")
 
 
+def agree(ok: bool, group=None) -> bool:
+    """True on every rank iff `ok` is true on every rank (one small MAX
+    all_reduce where the backend keeps its buffers)."""
+    flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=comm_device(group))
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    return int(flag.item()) == 0
+
+
 def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], map_shape,
-                  *, dtype=torch.float32, device=None, group=None):
+                  *, dtype=torch.float32, device=None, group=None,
+                  check: Callable[[], None] | None = None):
     """Runs `compute(pair) -> H x W map` on this rank's shard of `pairs` and
     gathers the maps to rank 0 (returned there, None elsewhere).
 
@@ -76,9 +85,14 @@ def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], ma
     stream (see PipelinedGather): the staging copy and the gather are
     ordered after that stream only.
 
-    Failures are agreed on before any gather: if `compute` raises or returns
-    a map of the wrong shape on any rank, every rank raises (a rank that
-    raised alone would leave the others blocked in the gather)."""
+    `check` (e.g. an SGM handle's `check`, sgm_check) runs after this rank's
+    frames: it waits for them and raises if a frame's maps are invalid (a
+    slanted-pass hand-off that gave up), so such a map is never gathered.
+
+    Failures are agreed on before any gather: if `compute` or `check` raises,
+    or `compute` returns a map of the wrong shape, on any rank, every rank
+    raises (a rank that raised alone would leave the others blocked in the
+    gather)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     h, w = map_shape
@@ -90,13 +104,14 @@ def process_batch(pairs: Sequence, compute: Callable[[object], torch.Tensor], ma
             if tuple(m.shape) != (h, w):
                 raise ValueError(f"compute returned a {tuple(m.shape)} map, expected {(h, w)}")
             mine.append(m)
+        if check is not None and mine:
+            check()
     except Exception as e:  # noqa: BLE001 -- re-raised below, on every rank
         err = e
-    flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=comm_device(group))
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    all_ok = agree(err is None, group)
     if err is not None:
         raise err
-    if int(flag.item()):
+    if not all_ok:
         raise RuntimeError("process_batch: compute failed on another rank")
     if mine:
         local = torch.stack([m.to(device=dev, dtype=dtype) for m in mine])
@@ -124,10 +139,22 @@ class PipelinedGather:
     torch.cuda.current_stream().cuda_stream)`, or make the handle's own stream
     current (`torch.cuda.set_stream(torch.cuda.ExternalStream(sgm.stream))`,
     as bench.py does).  `process_device(stream=None)` alone runs on the
-    handle's non-blocking stream, which torch's streams do not wait for."""
+    handle's non-blocking stream, which torch's streams do not wait for.
 
-    def __init__(self, shape, dtype, device, depth: int = 2, group=None):
+    Validity: `check` (e.g. the producing handle's `check`, sgm_check) is
+    called by `verify()` (and by `drain()` unless `verify=False`); a frame
+    whose maps are invalid (a slanted-pass hand-off that gave up) makes every
+    rank raise there.  `gathered()` returns only steps submitted before the
+    last successful verification, so a timed-out frame is never handed out
+    as valid.  The check is not made per submit: it waits for the frame,
+    which would serialise the host with the GPU and take away the overlap
+    this class exists for."""
+
+    def __init__(self, shape, dtype, device, depth: int = 2, group=None,
+                 check: Callable[[], None] | None = None):
         self.group = group
+        self.check = check
+        self.verified = 0  # steps [0, verified) passed verify()
         self.depth = depth
         world = dist.get_world_size(group)
         self.root = dist.get_rank(group) == 0
@@ -158,15 +185,38 @@ class PipelinedGather:
                                    async_op=True)
         self.k += 1
 
-    def drain(self) -> None:
+    def drain(self, verify: bool = True) -> None:
         for i, w in enumerate(self.work):
             if w is not None:
                 w.wait()
                 self.work[i] = None
+        if verify:
+            self.verify()
+
+    def verify(self) -> None:
+        """Collective: runs `check` on this rank and agrees on the result;
+        raises on every rank if any rank's frames since the last verification
+        are invalid."""
+        err = None
+        if self.check is not None:
+            try:
+                self.check()
+            except Exception as e:  # noqa: BLE001 -- re-raised below, on every rank
+                err = e
+        ok = agree(err is None, self.group)
+        if err is not None:
+            raise err
+        if not ok:
+            raise RuntimeError("PipelinedGather: a frame on another rank is invalid")
+        self.verified = self.k
 
     def gathered(self, step: int):
-        """Rank 0: the maps of `step` (valid after drain() and while fewer than
-        `depth` later steps have been submitted); None elsewhere."""
+        """Rank 0: the maps of `step` (complete once buffer() has come round to
+        its slot again, or after drain(), and while fewer than `depth` later
+        steps have been submitted); None elsewhere.  Raises for a step that no
+        successful verify() covers yet."""
+        if step >= self.verified:
+            raise RuntimeError(f"PipelinedGather: step {step} is not verified yet (drain() or verify())")
         return None if not self.root else self.recv[step % self.depth]
 
 

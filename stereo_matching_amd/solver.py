@@ -152,6 +152,13 @@ class SGM:
             sky_pitch or self.cols, ctypes.c_void_p(d_out), out_pitch or self.cols,
             ctypes.c_void_p(d_raw or None), _stream(stream)), self._h)
 
+    def check(self) -> None:
+        """sgm_check: wait for the frames enqueued so far and raise SGMError
+        (SGM_ERR_HIP) if a slanted-pass hand-off gave up in any of them since
+        the last report (their maps are invalid).  Call it after
+        synchronising and before gathering or timing device maps."""
+        check(self._lib.sgm_check(self._h), self._h)
+
     def get_disp(self) -> np.ndarray:
         """Post-filtered disparity (inc/Solver.h:36: filtered_disp after
         post_filter, Solver.cpp:600-649), computed on the GPU; invalid = D+1."""

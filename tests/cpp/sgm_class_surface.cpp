@@ -9,7 +9,12 @@
 //                                         OUT2 again after show_disp()
 //   sgm_class_surface sky IMG H W S OUT   -> SkyAreaDetector::detect mask
 //   sgm_class_surface lk L R DISP H W D OUT -> LKSubPixel::LKRefine of DISP
+//   sgm_class_surface batch PREFIX N H W D OUT -> BatchSGM over the devices of
+//                                         SGM_AMD_DEVICES (default "0"): pairs
+//                                         PREFIX_l<k>.raw / PREFIX_r<k>.raw, k < N,
+//                                         their get_disp() maps to OUT in pair order
 #define SGM_AMD_THROW 1
+#include "sgm_amd/BatchSGM.h"
 #include "sgm_amd/SGM.h"
 #include "sgm_amd/GPU_SGM.h"
 #include "sgm_amd/LKSubPixel.h"
@@ -39,6 +44,13 @@ int main(int argc, char **argv) {
         bad += expect_throw(375, 1242, 1, 48);   // d not allowed    (Solver.cpp:10)
         bad += expect_throw(0, 1242, 1, 64);     // h > 0            (Solver.cpp:6)
         bad += expect_throw(375, 1242, 1, 64);   // valid, but no GPU in this container
+        try {  // the multi-GPU batch: no device here either
+            sgm_amd::BatchSGM batch(std::vector<int>{0}, 375, 1242, 1, 64);
+            std::printf("BatchSGM did not throw\n");
+            ++bad;
+        } catch (const std::runtime_error &e) {
+            std::printf("BatchSGM threw: %s\n", e.what());
+        }
         Mat m(4, 5, CV_32FC1);
         m.at<float>(3, 4) = 2.5f;
         Mat shallow = m;
@@ -66,6 +78,40 @@ int main(int argc, char **argv) {
         std::ofstream fo(argv[7], std::ios::binary);
         for (int i = 0; i < disp.rows; ++i)
             fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
+        return fo ? 0 : 4;
+    }
+    if (argc == 8 && std::string(argv[1]) == "batch") {
+        const std::string prefix = argv[2];
+        const int n = std::atoi(argv[3]), h = std::atoi(argv[4]), w = std::atoi(argv[5]),
+                  d = std::atoi(argv[6]);
+        std::vector<int> devices;
+        const char *env = std::getenv("SGM_AMD_DEVICES");
+        for (const char *c = env && *env ? env : "0"; *c;) {
+            devices.push_back(std::atoi(c));
+            while (*c && *c != ',') ++c;
+            if (*c == ',') ++c;
+        }
+        std::vector<Mat> ls, rs;
+        for (int k = 0; k < n; ++k) {
+            Mat l(h, w, CV_8UC1), r(h, w, CV_8UC1);
+            std::ifstream fl(prefix + "_l" + std::to_string(k) + ".raw", std::ios::binary),
+                fr(prefix + "_r" + std::to_string(k) + ".raw", std::ios::binary);
+            fl.read(reinterpret_cast<char *>(l.data), (std::streamsize)h * w);
+            fr.read(reinterpret_cast<char *>(r.data), (std::streamsize)h * w);
+            if (!fl || !fr) return 2;
+            ls.push_back(l);
+            rs.push_back(r);
+        }
+        sgm_amd::BatchSGM batch(devices, h, w, 1, d);  // SGM(h, w, s, d) per device, node.cpp:49
+        batch.process(ls, rs);                         // node.cpp:93 for every pair
+        std::ofstream fo(argv[7], std::ios::binary);
+        for (int k = 0; k < n; ++k) {
+            const Mat &disp = batch.get_disp(k);       // node.cpp:104
+            if (disp.rows != h || disp.cols != w) return 3;
+            for (int i = 0; i < disp.rows; ++i)
+                fo.write(reinterpret_cast<const char *>(disp.ptr<float>(i)), (std::streamsize)w * 4);
+        }
+        std::printf("batch of %d pairs on %zu device(s)\n", n, devices.size());
         return fo ? 0 : 4;
     }
     if (argc == 10 && std::string(argv[1]) == "rungpu") {

@@ -52,3 +52,17 @@ def test_configs_cover_baseline():
     assert (c["k128"]["D"], c["k128"]["views"]) == (128, 1)
     assert (c["hd256"]["h"], c["hd256"]["w"], c["hd256"]["views"]) == (1080, 1920, 2)
     assert c["4k256full"].get("full") and c["4k256full"]["D"] == 256
+
+
+def test_gpus_must_match_world_size():
+    # a bench line must describe the ranks that ran: --gpus N without N ranks
+    # exits non-zero before touching a GPU (no WORLD_SIZE = one rank)
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode != 0
+    assert "--gpus 2 but WORLD_SIZE 1" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]

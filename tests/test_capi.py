@@ -118,3 +118,36 @@ def test_no_silent_fallback_without_gpu(lib):
     from stereo_matching_amd import SGM, SGMError
     with pytest.raises(SGMError):
         SGM(375, 1242, 1, 128)
+
+
+def test_check_and_comm_reject_null(lib):
+    # sgm_check and the multi-GPU exchange validate before touching a device
+    assert lib.sgm_check(None) == _capi.SGM_ERR_INVALID_ARG
+    h = ctypes.c_void_p()
+    assert lib.sgm_comm_create(None, 1, ctypes.byref(h)) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_comm_create((ctypes.c_int * 1)(0), 0, ctypes.byref(h)) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_comm_create((ctypes.c_int * 1)(0), 1, None) == _capi.SGM_ERR_INVALID_ARG
+    assert not h.value
+    assert lib.sgm_comm_create_rank(None, 1, 0, 0, ctypes.byref(h)) == _capi.SGM_ERR_INVALID_ARG
+    uid = b"\0" * _capi.SGM_COMM_ID_BYTES
+    assert lib.sgm_comm_create_rank(uid, 2, 2, 0, ctypes.byref(h)) == _capi.SGM_ERR_INVALID_ARG
+    assert b"nranks or rank" in lib.sgm_comm_last_error(None)
+    assert lib.sgm_comm_create_rank(uid, 0, 0, 0, ctypes.byref(h)) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_comm_unique_id(None) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_comm_destroy(None) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_comm_info(None, None, None, None) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_batch_gather(None, 0, None, 1, 1, 1, None, None) == _capi.SGM_ERR_INVALID_ARG
+    assert lib.sgm_batch_gather_all(None, None, 1, 1, 1, None, None) == _capi.SGM_ERR_INVALID_ARG
+
+
+def test_comm_without_gpu(lib):
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    h = ctypes.c_void_p()
+    # (a duplicated device list: no device, or refused as a duplicate)
+    rc = lib.sgm_comm_create((ctypes.c_int * 2)(0, 0), 2, ctypes.byref(h))
+    assert rc in (_capi.SGM_ERR_NO_DEVICE, _capi.SGM_ERR_INVALID_ARG)
+    assert lib.sgm_comm_create((ctypes.c_int * 1)(0), 1, ctypes.byref(h)) == _capi.SGM_ERR_NO_DEVICE
+    assert b"no HIP device" in lib.sgm_comm_last_error(None)
+    assert not h.value

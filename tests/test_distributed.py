@@ -115,6 +115,8 @@ def _pipe_worker(rank, world, port, q):
         seen = {}
         for k in range(5):
             buf = pipe.buffer()            # waits for the gather of step k-2
+            if k >= 2:
+                pipe.verify()              # collective: every rank's frames so far are valid
             if k >= 2 and rank == 0:       # step k-2's maps are complete now
                 seen[k - 2] = [t.clone().numpy() for t in pipe.gathered(k - 2)]
             buf.fill_(100 * rank + k)      # "compute" step k into the buffer

@@ -65,19 +65,20 @@ os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 assert dist.get_backend() == "nccl"
 want = [single(p) for p in PAIRS]
-batch = sd.process_batch(PAIRS, compute, (H, W))
+batch = sd.process_batch(PAIRS, compute, (H, W), check=sgm.check)
 assert batch.is_cuda and tuple(batch.shape) == (5, H, W)
 for k in range(5):
     assert same(batch[k], want[k]), k
 print("process_batch ok", flush=True)
 # bench.py's overlapped gather: step k writes buffer k % 2 while step k-1's
 # gather may still run; each step's gathered map must be that step's pair
-pipe = sd.PipelinedGather((H, W), torch.float32, dev, depth=2)
+pipe = sd.PipelinedGather((H, W), torch.float32, dev, depth=2, check=sgm.check)
 dl = [torch.from_numpy(p[0]).to(dev) for p in PAIRS]
 dr = [torch.from_numpy(p[1]).to(dev) for p in PAIRS]
 for k in range(6):
     buf = pipe.buffer()
     if k >= 2:
+        pipe.verify()
         assert same(pipe.gathered(k - 2)[0], want[(k - 2) % 5]), k - 2
     sgm.process_device(dl[k % 5].data_ptr(), dr[k % 5].data_ptr(), buf.data_ptr(),
                        stream=stream.cuda_stream)
@@ -96,11 +97,13 @@ rank = int(sys.argv[3])
 dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=rank,
                         world_size=2)
 pairs = PAIRS[:3]                       # uneven: rank 0 holds pairs 0, 2; rank 1 pair 1
-batch = sd.process_batch(pairs, compute, (H, W))
-pipe = sd.PipelinedGather((H, W), torch.float32, dev, depth=2)
+batch = sd.process_batch(pairs, compute, (H, W), check=sgm.check)
+pipe = sd.PipelinedGather((H, W), torch.float32, dev, depth=2, check=sgm.check)
 seen = {}
 for k in range(4):
     buf = pipe.buffer()
+    if k >= 2:
+        pipe.verify()
     if k >= 2 and rank == 0:
         seen[k - 2] = [t.clone() for t in pipe.gathered(k - 2)]
     p = PAIRS[(2 * k + rank) % 5]       # rank r's pair of step k
@@ -150,17 +153,19 @@ def compute(pair):
     m = torch.empty((H, W), dtype=torch.float32, device=dev)
     sgm.process_device(l.data_ptr(), r.data_ptr(), m.data_ptr(), stream=stream.cuda_stream)
     return m
-batch = sd.process_batch(PAIRS, compute, (H, W))
+batch = sd.process_batch(PAIRS, compute, (H, W), check=sgm.check)
 # bench.py's batched gather (--gather-every 4): step k of rank r computes pair
 # (k + r) % 8 into slot k % 4 of the rotating (4, H, W) buffer; one gather per
 # 4 steps, overlapped with the next 4
-pipe = sd.PipelinedGather((GK, H, W), torch.float32, dev, depth=2)
+pipe = sd.PipelinedGather((GK, H, W), torch.float32, dev, depth=2, check=sgm.check)
 dl = [torch.from_numpy(p[0]).to(dev) for p in PAIRS]
 dr = [torch.from_numpy(p[1]).to(dev) for p in PAIRS]
 got = {}
 for k in range(3 * GK):
     if k % GK == 0:
         buf = pipe.buffer()
+        if k >= 2 * GK:
+            pipe.verify()
         if k >= 2 * GK and rank == 0:
             got[k // GK - 2] = [t.clone() for t in pipe.gathered(k // GK - 2)]
     p = (k + rank) % N
@@ -277,6 +282,11 @@ def test_bench_under_torch_distributed_run(extra):
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     rec = json.loads(line)
     assert rec["n_gpus"] == 1 and rec["value"] > 0
+    # what the process group saw, for the driver's SCALE runs to check
+    assert rec["backend"] == "nccl" and rec["world_size_seen"] == 1
+    assert 0 < rec["rank_timed_s"]["min"] <= rec["rank_timed_s"]["max"]
+    assert abs(rec["rank_timed_s"]["max"] * 1e3 / 5 - rec["ms_per_step"]) < 1e-3 * rec["ms_per_step"] + 1e-3
+    assert rec["frames_verified"] == ["warmup", "timed"]
     assert "RCCL" in rec["config"]["parallelism"]
     par = rec["config"]["parallelism"]
     if extra == ["--gather-every", "3"]:

@@ -10,7 +10,7 @@ SRC=$ROOT/build/${NAME}_src
 rm -rf "$SRC"
 mkdir -p "$SRC" "$ROOT/build/$NAME"
 cp "$ROOT"/stereo_matching_amd/csrc/*.hip "$ROOT"/stereo_matching_amd/csrc/*.h "$ROOT"/stereo_matching_amd/csrc/Makefile "$SRC"/
-make -s -C "$SRC" -j8 OUT="$ROOT/build/$NAME/libsgm_hip.so" \
+make -s -C "$SRC" -j8 OUT="$ROOT/build/$NAME/libsgm_hip.so" "$ROOT/build/$NAME/libsgm_hip.so" \
   HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fno-honor-nans -mno-amdgpu-ieee -Wall -Wno-unused-result -I$ROOT/include $FLAGS"
 rm -f "$SRC"/*.o
 echo "built build/$NAME/libsgm_hip.so ($FLAGS)"
