@@ -216,6 +216,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 
         if (wave == NW) {
             // ----------------------------------------------- receiver wave
+#ifdef SLANT_RECV_PRIO
+            __builtin_amdgcn_s_setprio(SLANT_RECV_PRIO);
+#endif
             // Phase p = 0 .. nsteps (the prologue, then one per step; each
             // ends on the tile's barrier) hands the next tile's exit states
             // of step gs = s_begin - 1 + p to LDS parity gs & 1 (slots NW,
