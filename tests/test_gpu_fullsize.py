@@ -55,7 +55,8 @@ def _config5_images(h, w, pair_index):
 @pytest.mark.timeout(600)
 def test_4k256_lr_vs_lean_oracle():
     """Both views of config 5's frame with the synthetic sky masks (rows <
-    H/6), the default banded schedule, against orc_process_lean: WTA
+    H/6), the default schedule (slanted tiles at this size, sgm_capi.hip
+    slant_default), against orc_process_lean: WTA
     disparities of both views, F_R and the LR-checked map, bit for bit.  The
     frame contains pixels where the parabola's denominator (a+b)-2c rounds to
     0 (Solver.cpp:589: x = +inf -> std::min -> D-1 while disp < D-1)."""
