@@ -142,6 +142,20 @@ static __device__ unsigned long long slant_stamps[32];
 #define SLANT_STAMP(i, v) atomicAdd(&slant_stamps[(UP ? 16 : 0) + (i)], (unsigned long long)(v))
 #endif
 
+#ifdef SGM_SLANT_HOPS
+// Hop timeline (tools/slant_hops.py): per pass and (view, tile, step), in
+// s_memrealtime ticks (100 MHz, chip-wide), low 32 bits: [0] compute wave 0
+// issued this tile's exit-state stores of the step, [1] the receiver started
+// the phase that needs the next tile's states of the step, [2] it held them,
+// [3] compute wave 0 left the barrier that ends the step.
+constexpr size_t kHopN = (size_t)1 << 21;
+static __device__ unsigned slant_hops[2][4][kHopN];
+__device__ __forceinline__ void hop_mark(int pass, int what, int T, int H, int view, int t, int s) {
+    const size_t i = ((size_t)view * T + t) * H + s;
+    if (s >= 0 && i < kHopN) slant_hops[pass][what][i] = (unsigned)__builtin_amdgcn_s_memrealtime();
+}
+#endif
+
 // Exit states of a tile per step, as (wave, exchanged-state index) pairs:
 // bottom-up (w0 L4, w0 L8, w1 L8), top-down (w0 L6, w1 L6).
 template <bool UP>
@@ -248,6 +262,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             auto phase = [&](int slot, int p) {
                 const int gs = s_begin - 1 + p;
                 const bool want = gvalid(p);
+#ifdef SGM_SLANT_HOPS
+                if (lane == 0 && want) hop_mark(UP, 1, T, H, view, t, gs);
+#endif
                 const int c0 = u_lo + NW + gs;  // tile t+1's wave 0 column at step gs
                 bool need[NX];
 #pragma unroll
@@ -309,6 +326,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     rp_ticks += __builtin_amdgcn_s_memtime() - sp0;
 #endif
                 }
+#ifdef SGM_SLANT_HOPS
+                if (lane == 0 && want) hop_mark(UP, 2, T, H, view, t, gs);
+#endif
                 // (a phase with nothing wanted writes slots that no valid
                 // predecessor reads)
                 const int par = gs & 1;
@@ -463,6 +483,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     for (int v = 0; v < V; ++v) xa[v] = k == 0 ? L4[v] : L2[v];
                     store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, xa, tag);
                     store_granules<V>(xrs_b, (s * 3 + 1) * D * 8 + goff, L2, tag);
+#ifdef SGM_SLANT_HOPS
+                    if (k == 0 && lane == 0) hop_mark(1, 0, T, H, view, t, s);
+#endif
                 }
                 const float n4 = wave_min(lane_min(L4));
                 // ((S12 + L3) + L4) + ((T56 + L7) + L8)
@@ -478,6 +501,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 pstep = s;
             } else {
                 store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, L2, tag);
+#ifdef SGM_SLANT_HOPS
+                if (k == 0 && lane == 0) hop_mark(0, 0, T, H, view, t, s);
+#endif
                 // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
                 float o[V];
 #pragma unroll
@@ -499,6 +525,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #ifdef SGM_SLANT_STAMPS
             st_prev = __builtin_amdgcn_s_memtime();
             st_wait += st_prev - tb0;
+#endif
+#ifdef SGM_SLANT_HOPS
+            if (k == 0 && lane == 0) hop_mark(UP, 3, T, H, view, t, s);
 #endif
         };
         int s0 = s_begin;
@@ -589,6 +618,28 @@ hipError_t launch_slant_up(const SlantArgs &a, Geom g, hipStream_t st) { return 
 hipError_t launch_slant_down(const SlantArgs &a, Geom g, hipStream_t st) { return launch_slant_t<false>(a, g, st); }
 
 }  // namespace sgm
+
+#ifdef SGM_SLANT_HOPS
+// the hop timeline of both passes (tools/slant_hops.py): out holds
+// 2 x 4 x n words (n <= 2^21, entries (view * T + t) * H + s); reset clears it
+extern "C" int sgm_debug_slant_hops(unsigned *out, size_t n, int reset) {
+    if (n > sgm::kHopN) return -1;
+    for (int p = 0; p < 2; ++p)
+        for (int w = 0; w < 4; ++w) {
+            const size_t off = ((size_t)p * 4 + w) * sgm::kHopN * sizeof(unsigned);
+            if (out && hipMemcpyFromSymbol(out + ((size_t)p * 4 + w) * n, HIP_SYMBOL(sgm::slant_hops),
+                                           n * sizeof(unsigned), off) != hipSuccess)
+                return -1;
+        }
+    if (reset) {
+        void *ptr = nullptr;
+        if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(sgm::slant_hops)) != hipSuccess ||
+            hipMemset(ptr, 0, sizeof(sgm::slant_hops)) != hipSuccess)
+            return -1;
+    }
+    return 0;
+}
+#endif
 
 #ifdef SGM_SLANT_STAMPS
 extern "C" int sgm_debug_slant_stamps(unsigned long long *out, int reset) {

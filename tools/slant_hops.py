@@ -1,0 +1,100 @@
+"""Hop timeline of the slanted passes: when each tile's
+exit states were stored, when the next tile's receiver needed and held them,
+and when each step's barrier was left (s_memrealtime, 100 MHz, chip-wide).
+
+Library built with -DSGM_SLANT_HOPS (bash tools/variant.sh hops
+-DSGM_SLANT_HOPS), loaded with SGM_HIP_LIB=build/hops/libsgm_hip.so.
+Usage (GPU): python tools/slant_hops.py [H W D V]   (default HD256, two views)
+
+Printed per pass:
+  * hop: held(t, s) - stored(t+1, s), the producer's store to the consumer
+    holding the states, over the phases in which the receiver had to wait
+    (held - needed > 0.2 us) and over all phases;
+  * wait: held - needed, the time the receiver's phase waited for the hop;
+  * step: barrier(t, s) - barrier(t, s-1), the tile's step period, split by
+    whether the step's input hop made the receiver wait;
+  * lag: barrier(t, s) - barrier(t+1, s-1), how far a tile runs behind its
+    producer."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["SGM_SLANT"] = "1"
+import torch  # noqa: E402
+
+from stereo_matching_amd import SGM, _capi, synthetic  # noqa: E402
+
+NW = 14
+
+
+def pct(x):
+    if x.size == 0:
+        return "n/a"
+    q = np.percentile(x, [10, 50, 90])
+    return f"p10 {q[0]:6.2f}  p50 {q[1]:6.2f}  p90 {q[2]:6.2f}  mean {x.mean():6.2f} us  (n={x.size})"
+
+
+def main():
+    h, w, D, V = (int(x) for x in sys.argv[1:5]) if len(sys.argv) > 4 else (1080, 1920, 256, 2)
+    left, right = synthetic.stereo_pair(h, w, D, pair_index=0)
+    dev = torch.device("cuda", 0)
+    dl, dr = torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev)
+    out = torch.empty((h, w), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    sgm = SGM(h, w, 1, D, views=V, device=0)
+    lib = _capi.lib()
+    lib.sgm_debug_slant_hops.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    T = (w + h - 1 + NW - 1) // NW
+    n = V * T * h
+    for _ in range(3):
+        sgm.process_device(dl.data_ptr(), dr.data_ptr(), out.data_ptr())
+    sgm.check()
+    assert lib.sgm_debug_slant_hops(None, n, 1) == 0
+    sgm.set_profiling(True)
+    sgm.process_device(dl.data_ptr(), dr.data_ptr(), out.data_ptr())
+    sgm.check()
+    prof = sgm.get_profile()
+    buf = np.zeros((2, 4, n), np.uint32)
+    assert lib.sgm_debug_slant_hops(buf.ctypes.data, n, 0) == 0
+    print(f"{w}x{h} D={D} V={V}: {T} tiles per view; slant_down {prof['slant_down'][1]:.3f} ms, "
+          f"slant_up {prof['slant_up'][1]:.3f} ms")
+    for p, name in ((0, "top-down"), (1, "bottom-up")):
+        a = buf[p].reshape(4, V, T, h).astype(np.int64)
+        have = a != 0
+        t0 = a[have].min()
+
+        def us(x):
+            return (x % (1 << 32)).astype(np.float64) / 100.0  # ticks (10 ns) -> us
+
+        st, nd, hd, br = a[0], a[1], a[2], a[3]
+        # consumer tile t, step s needs producer tile t+1's step s (its exit states)
+        ok = have[1][:, :-1, :] & have[2][:, :-1, :] & have[0][:, 1:, :]
+        hop = us((hd[:, :-1, :] - st[:, 1:, :]) % (1 << 32))[ok]
+        wait = us((hd[:, :-1, :] - nd[:, :-1, :]) % (1 << 32))[ok]
+        waited = wait > 0.2
+        print(f"  {name}: span {us(np.array([a[have].max() - t0]))[0]:.0f} us, phases {ok.sum()}, "
+              f"receiver waited in {waited.mean() * 100:.1f}%")
+        print(f"    hop  (waited) {pct(hop[waited])}")
+        print(f"    hop  (all)    {pct(hop)}")
+        print(f"    wait (waited) {pct(wait[waited])}")
+        # step periods: barrier(t, s) - barrier(t, s-1); the input of step s is
+        # the hand-off of step s-1 (phase gs = s-1)
+        okb = have[3][:, :, 1:] & have[3][:, :, :-1]
+        per = us((br[:, :, 1:] - br[:, :, :-1]) % (1 << 32))
+        wmask = np.zeros_like(okb)
+        wfull = np.zeros(have[1].shape, bool)
+        wfull[:, :-1, :] = ok & (us((hd[:, :-1, :] - nd[:, :-1, :]) % (1 << 32)) > 0.2)
+        wmask[:, :, :] = wfull[:, :, :-1]
+        print(f"    step (input hop waited) {pct(per[okb & wmask])}")
+        print(f"    step (input was ready)  {pct(per[okb & ~wmask])}")
+        okl = have[3][:, :-1, 1:] & have[3][:, 1:, :-1]
+        lag = us((br[:, :-1, 1:] - br[:, 1:, :-1]) % (1 << 32))
+        lag = np.where(lag > 2 ** 31 / 100, lag - 2 ** 32 / 100, lag)
+        print(f"    lag behind the producer tile {pct(lag[okl])}")
+
+
+if __name__ == "__main__":
+    main()
