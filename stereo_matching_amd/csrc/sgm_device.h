@@ -104,6 +104,44 @@ __device__ __forceinline__ float wave_min(float x) {
 // Same value (kept for call sites that want the name).
 __device__ __forceinline__ float wave_min_u(float x) { return wave_min(x); }
 
+// wave_min of N independent values, stage by stage: each DPP stage of one
+// value issues between two of another's, so the VALU-write -> DPP-read wait
+// states are filled with work instead of s_nop (one reduction's latency for N
+// results).  Exact like wave_min: min is exact, so the order is free.
+template <int N>
+__device__ __forceinline__ void wave_min_n(float (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = fminf(x[i], movdppf<DPP_QP_1032>(x[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = fminf(x[i], movdppf<DPP_QP_2301>(x[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = fminf(x[i], movdppf<DPP_HALF_MIRROR>(x[i]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = fminf(x[i], movdppf<DPP_MIRROR>(x[i]));
+    static_assert(N == 2 || N == 3, "wave_min_n: 2 or 3 values");
+    // (N >= 2 instructions between a value's two row_bcast steps give its
+    // second read one wait state; the s_nop 0 adds the other)
+    if constexpr (N == 2)
+        asm("s_nop 1\n\t"
+            "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "v_min_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "s_nop 0\n\t"
+            "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+            "v_min_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+            : "+v"(x[0]), "+v"(x[1]));
+    else
+        asm("s_nop 1\n\t"
+            "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "v_min_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "v_min_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+            "v_min_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+            "v_min_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf"
+            : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 63));
+}
+
 // min(src of the neighbouring lane, a): SHR reads lane l-1, SHL lane l+1.
 // The edge lane (0 for SHR, 63 for SHL) has no source: with bound_ctrl off
 // the DPP op is disabled there and the tied destination keeps a.

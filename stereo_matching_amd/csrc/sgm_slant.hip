@@ -332,14 +332,22 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 // (a phase with nothing wanted writes slots that no valid
                 // predecessor reads)
                 const int par = gs & 1;
+                // the states to LDS, then their minima, all NX reductions
+                // interleaved (this phase ends the tile's step: it sits on
+                // the tile-to-tile hop)
+                float mx[NX];
 #pragma unroll
                 for (int x = 0; x < NX; ++x) {
                     float yy[V];
 #pragma unroll
                     for (int v = 0; v < V; ++v) yy[v] = dact ? y[x][v] : SGM_INF;
-                    const float m = wave_min(lane_min(yy));
+                    mx[x] = lane_min(yy);
                     store_lds_v<V>(&L.st[par][NW + X::wave(x)][X::kind(x)][e0], yy);
-                    if (lane == 0) L.pm[par][NW + X::wave(x)][X::kind(x)] = m;
+                }
+                wave_min_n<NX>(mx);
+                if (lane == 0) {
+#pragma unroll
+                    for (int x = 0; x < NX; ++x) L.pm[par][NW + X::wave(x)][X::kind(x)] = mx[x];
                 }
                 issue(slot, p + CR);
 #ifdef SGM_SLANT_STAMPS
@@ -453,41 +461,56 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             // yield L = C (P1, P2 >= 0)
             const bool v1 = s >= 1, vo = s >= 1 && j >= 1, v2 = s >= 1 && j + 1 <= W - 1;
             const float(&c)[V] = rb[0][q];
-            float q2[V], zo[V];
-            load_lds_v<V>(q2, &L.st[pp][k + 2][K2][e0]);
-            // (uniform LDS words: into SGPRs, dp_step's scalar operand)
-            float m2 = uni_f(L.pm[pp][k + 2][K2]);
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                q2[v] = v2 ? q2[v] : 0.0f;
-                zo[v] = vo ? po[v] : 0.0f;
-            }
-            m2 = v2 ? m2 : 0.0f;
-            const float mmo = vo ? mo : 0.0f;
-            float Lo[V], L2[V];
-            dp_step<V>(zo, mmo, c, Lo, a.p1, p2v);
-            dp_step<V>(q2, m2, c, L2, a.p1, p2v);
-            const float no = wave_min(lane_min(Lo)), n2 = wave_min(lane_min(L2));
+            // The exit states first (bottom-up L4 and L8, top-down L6): the
+            // next tile's step waits for them, so they are computed and
+            // stored before the own chain and the minima
+            float Lo[V], L2[V], L4[V];
             if constexpr (UP) {
                 float q1[V];
                 load_lds_v<V>(q1, &L.st[pp][k + 1][0][e0]);
+                // (uniform LDS words: into SGPRs, dp_step's scalar operand)
                 float m1 = uni_f(L.pm[pp][k + 1][0]);
 #pragma unroll
                 for (int v = 0; v < V; ++v) q1[v] = v1 ? q1[v] : 0.0f;
                 m1 = v1 ? m1 : 0.0f;
-                float L4[V];
                 dp_step<V>(q1, m1, c, L4, a.p1, p2v);
-                {
-                    float xa[V];
+            }
+            {
+                float q2[V];
+                load_lds_v<V>(q2, &L.st[pp][k + 2][K2][e0]);
+                float m2 = uni_f(L.pm[pp][k + 2][K2]);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) xa[v] = k == 0 ? L4[v] : L2[v];
-                    store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, xa, tag);
-                    store_granules<V>(xrs_b, (s * 3 + 1) * D * 8 + goff, L2, tag);
+                for (int v = 0; v < V; ++v) q2[v] = v2 ? q2[v] : 0.0f;
+                m2 = v2 ? m2 : 0.0f;
+                dp_step<V>(q2, m2, c, L2, a.p1, p2v);
+            }
+            if constexpr (UP) {
+                float xa[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) xa[v] = k == 0 ? L4[v] : L2[v];
+                store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, xa, tag);
+                store_granules<V>(xrs_b, (s * 3 + 1) * D * 8 + goff, L2, tag);
 #ifdef SGM_SLANT_HOPS
-                    if (k == 0 && lane == 0) hop_mark(1, 0, T, H, view, t, s);
+                if (k == 0 && lane == 0) hop_mark(1, 0, T, H, view, t, s);
 #endif
-                }
-                const float n4 = wave_min(lane_min(L4));
+            } else {
+                store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, L2, tag);
+#ifdef SGM_SLANT_HOPS
+                if (k == 0 && lane == 0) hop_mark(0, 0, T, H, view, t, s);
+#endif
+            }
+            float zo[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) zo[v] = vo ? po[v] : 0.0f;
+            const float mmo = vo ? mo : 0.0f;
+            dp_step<V>(zo, mmo, c, Lo, a.p1, p2v);
+            float no, n2;
+            if constexpr (UP) {
+                float mm[3] = {lane_min(L4), lane_min(L2), lane_min(Lo)};
+                wave_min_n<3>(mm);
+                const float n4 = mm[0];
+                n2 = mm[1];
+                no = mm[2];
                 // ((S12 + L3) + L4) + ((T56 + L7) + L8)
                 float tot[V];
 #pragma unroll
@@ -500,10 +523,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 for (int v = 0; v < V; ++v) ptot[v] = tot[v];
                 pstep = s;
             } else {
-                store_granules<V>(xrs_a, (s * 3 + xslot_a) * D * 8 + goff, L2, tag);
-#ifdef SGM_SLANT_HOPS
-                if (k == 0 && lane == 0) hop_mark(0, 0, T, H, view, t, s);
-#endif
+                float mm[2] = {lane_min(L2), lane_min(Lo)};
+                wave_min_n<2>(mm);
+                n2 = mm[0];
+                no = mm[1];
                 // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
                 float o[V];
 #pragma unroll

@@ -94,6 +94,15 @@ def main():
         lag = us((br[:, :-1, 1:] - br[:, 1:, :-1]) % (1 << 32))
         lag = np.where(lag > 2 ** 31 / 100, lag - 2 ** 32 / 100, lag)
         print(f"    lag behind the producer tile {pct(lag[okl])}")
+        # the hop loop: producer barrier(t+1, s-1) -> its exit-state stores
+        # (d1) -> consumer holds them (hop) -> consumer barrier(t, s) (d3)
+        okd = have[0][:, :, 1:] & have[3][:, :, :-1]
+        d1 = us((st[:, :, 1:] - br[:, :, :-1]) % (1 << 32))[okd]
+        okh = have[2] & have[3]
+        d3 = us((br - hd) % (1 << 32))[okh]
+        d3 = d3[d3 < 1000]
+        print(f"    d1 barrier -> exit stores issued {pct(d1)}")
+        print(f"    d3 held -> barrier left          {pct(d3)}")
 
 
 if __name__ == "__main__":
