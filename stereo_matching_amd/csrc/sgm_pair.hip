@@ -332,7 +332,10 @@ static void launch_vfwd2_l3_t(const float *const *in, float *const *out, const P
     if (g.D == 32) vfwd2_l3_kernel<1, false, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
     else if (g.D == 64) vfwd2_l3_kernel<1, true, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
     else if (g.D == 128) vfwd2_l3_kernel<2, true, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
-    else vfwd2_l3_kernel<4, true, WIN, 8><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+#ifndef VFWD2_PF4
+#define VFWD2_PF4 8
+#endif
+    else vfwd2_l3_kernel<4, true, WIN, VFWD2_PF4><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
 }
 
 hipError_t launch_vfwd2_l3(const float *const *in, float *const *out, float *const *l3, const PairArgs *a,

@@ -27,3 +27,18 @@ def test_slant_guard_and_small_grids():
     assert rec["recovery"] == {"exact": True, "check_ok": True}
     assert all(v["exact"] for v in rec["grids"].values()), rec["grids"]
     assert r.returncode == 0
+
+
+@pytest.mark.gpu
+def test_bench_refuses_invalid_frames():
+    # bench.py checks every pass's frames (sgm_check) before it reports a
+    # time: with a forced hand-off stall (debug build, slanted schedule
+    # forced on the K128 frame) it prints no JSON line and exits 3
+    env = {**os.environ, "SGM_HIP_LIB": os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so"),
+           "SGM_SLANT": "1", "SGM_SLANT_STALL": "20", "SGM_SLANT_SPIN_LIMIT": "2000"}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-profile-pass"],
+                       capture_output=True, text=True, timeout=180, cwd=ROOT, env=env)
+    assert r.returncode == 3, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "the warmup pass produced invalid frames" in r.stderr and "timed out" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
