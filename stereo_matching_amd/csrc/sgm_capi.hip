@@ -620,7 +620,13 @@ int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, i
 // the top-down pass's share of the CUs (eighths) while the H pair runs
 // beside it: measured best at 4/8 for D = 256 and 6/8 for D = 128 (HD256,
 // 4K256 one and two views, 4K128: profiles/r04_experiments/slant.txt)
-int slant_down_grid_eighths(int D) { return D >= 256 ? 4 : 6; }
+int slant_down_grid_eighths(int D) {
+#ifdef SGM_SLANT_DEBUG
+    if (const char *e = getenv("SGM_SLANT_DOWN_EIGHTHS"))  // share sweeps (tools/slant_share.sh)
+        if (atoi(e) >= 1 && atoi(e) <= 8) return atoi(e);
+#endif
+    return D >= 256 ? 4 : 6;
+}
 int slant_cus() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
