@@ -230,9 +230,13 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 
         if (wave == NW) {
             // ----------------------------------------------- receiver wave
-#ifdef SLANT_RECV_PRIO
-            __builtin_amdgcn_s_setprio(SLANT_RECV_PRIO);
+            // the receiver's phase ends every step of the tile: issue
+            // priority over the compute waves (HD256 slant_up -7%, 4K256
+            // -4..7%: profiles/r05_experiments/r05d_ab_*.txt)
+#ifndef SLANT_RECV_PRIO
+#define SLANT_RECV_PRIO 3
 #endif
+            __builtin_amdgcn_s_setprio(SLANT_RECV_PRIO);
             // Phase p = 0 .. nsteps (the prologue, then one per step; each
             // ends on the tile's barrier) hands the next tile's exit states
             // of step gs = s_begin - 1 + p to LDS parity gs & 1 (slots NW,
