@@ -618,14 +618,18 @@ int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, i
 //   slant_up (both views): L4, L7, L8 walking up, total
 //     ((S12 + L3) + L4) + ((T56 + L7) + L8), WTA, sub-pixel (row-major maps)
 // the top-down pass's share of the CUs (eighths) while the H pair runs
-// beside it: measured best at 4/8 for D = 256 and 6/8 for D = 128 (HD256,
-// 4K256 one and two views, 4K128: profiles/r04_experiments/slant.txt)
-int slant_down_grid_eighths(int D) {
+// beside it, so that the two finish together: round 5 (the receiver at
+// issue priority, exit states first) moved the best share up at D = 256:
+// HD256 two views 7/8 (12.75 vs 13.09 ms per frame at 4/8), 4K256 two views
+// 6/8 (43.7 vs 44.9; 7/8 44.4): profiles/r05_experiments/r05e_share_*.txt.
+// D = 128 keeps round 4's 6/8 (4K128, HD128: profiles/r04_experiments/slant.txt)
+int slant_down_grid_eighths(Geom g, int nviews) {
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_DOWN_EIGHTHS"))  // share sweeps (tools/slant_share.sh)
         if (atoi(e) >= 1 && atoi(e) <= 8) return atoi(e);
 #endif
-    return D >= 256 ? 4 : 6;
+    if (g.D >= 256) return nviews * g.W <= 4096 ? 7 : 6;
+    return 6;
 }
 int slant_cus() {
     int dev = 0, cus = 0;
@@ -692,7 +696,7 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     // (profiled as one more entry, "slant_down_hpair": fork to join on the
     // frame's stream, the pair's wall time; the two launches' own entries
     // overlap in time)
-    sa.max_grid = slant_down_grid_eighths(g.D) * slant_cus() / 8;
+    sa.max_grid = slant_down_grid_eighths(g, nv) * slant_cus() / 8;
     HIPCHK(h, timed(h, "slant_down_hpair", nv * elems, st, [&] {
         hipError_t e = hipEventRecord(h->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->st_h, h->ev_fork, 0);
