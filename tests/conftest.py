@@ -19,3 +19,19 @@ def oracle_lib():
     import oracle
     oracle.build()
     return oracle
+
+
+def pytest_sessionstart(session):
+    # GPU sessions: initialise PyTorch's HIP runtime before anything loads
+    # libsgm_hip.so.  The process then holds two HIP runtimes (PyTorch's
+    # bundled one and /opt/rocm's, which the library links); PyTorch's finds
+    # no GPU when the other initialised first, so the tests that use torch
+    # device tensors depend on this order, as bench.py does.
+    expr = session.config.getoption("markexpr", "") or ""
+    if "gpu" in expr and "not gpu" not in expr:
+        try:
+            import torch
+            if torch.cuda.device_count() > 0:
+                torch.cuda.init()
+        except Exception:
+            pass
