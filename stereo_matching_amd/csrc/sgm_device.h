@@ -657,13 +657,16 @@ __device__ __forceinline__ int group_min_i(int x) {
 // address arithmetic.
 // sub goes to sub_top + sub_off (its own layout: column-major maps of the
 // two-view frames), disp to pix_top + pix_off (row-major).
-// The core of the batched WTA: this lane's QQ totals x (disparities d0 ..
-// d0+QQ-1 of one pixel, LPP lanes per pixel) and the pixel's LDS row (the
-// sub-pixel's neighbours) give the pixel's disparity d and sub-pixel value f
-// in every lane of the group.
-template <int LPP, int QQ>
-__device__ __forceinline__ void wta_q_core(const float (&x)[QQ], const float *row, int d0, int Dn,
-                                           float uniq, int &d_out, float &f_out) {
+template <int V, int PF, int QQ>
+__device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*tb)[tbuf_stride<V>()],
+                                            long long pix_top, unsigned pix_off, long long sub_top,
+                                            unsigned sub_off, int cnt, int lane, int Dn, float uniq,
+                                            uint16_t *disp, float *sub) {
+    constexpr int LPP = 64 / PF;  // lanes per pixel
+    static_assert(QQ % 4 == 0 && LPP <= 32, "QQ a multiple of 4, at most 32 lanes per pixel");
+    const int px = lane / LPP, q = lane - px * LPP;
+    const int d0 = q * QQ;
+    const float *row = tb[px < cnt ? px : 0];
     float lm = x[0];
 #pragma unroll
     for (int k = 1; k < QQ; ++k) lm = fminf(lm, x[k]);
@@ -698,91 +701,6 @@ __device__ __forceinline__ void wta_q_core(const float (&x)[QQ], const float *ro
         const float lim = (Dn - 1) * 1.f;
         f = (lim < xx) ? lim : xx;  // std::min(x, lim)
     }
-    d_out = d;
-    f_out = f;
-}
-
-// The same, reading the lane's QQ totals from the pixel's LDS row in each of
-// its three passes (min; first index of m and the smallest other value;
-// first index of that value) instead of holding them in registers: for
-// callers at the register limit (the slanted bottom-up pass).  The compiler
-// barriers make each pass re-read LDS rather than keep the first pass's
-// values live.
-template <int LPP, int QQ>
-__device__ __forceinline__ void wta_q_core_lds(const float *row, int d0, int Dn, float uniq,
-                                               int &d_out, float &f_out) {
-    const float *xr = row + d0;
-    auto rd = [&](int k4, float (&x)[4]) {
-        const float4 v = *reinterpret_cast<const float4 *>(xr + k4);
-        x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-    };
-    float lm = SGM_INF;
-#pragma unroll
-    for (int k4 = 0; k4 < QQ; k4 += 4) {
-        float x[4];
-        rd(k4, x);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) lm = fminf(lm, x[e]);
-    }
-    const float m = group_min<LPP>(lm);
-    asm volatile("" ::: "memory");
-    int li = QQ;
-    float ls = SGM_INF;
-#pragma unroll
-    for (int k4 = QQ - 4; k4 >= 0; k4 -= 4) {
-        float x[4];
-        rd(k4, x);
-#pragma unroll
-        for (int e = 3; e >= 0; --e) {
-            const bool eq = x[e] == m;
-            li = eq ? k4 + e : li;
-            ls = eq ? ls : fminf(ls, x[e]);
-        }
-    }
-    const int mi = group_min_i<LPP>(li < QQ ? d0 + li : INT_MAX);
-    const float sec = group_min<LPP>(ls);
-    int d = mi;
-    if (sec != SGM_INF) {  // a second distinct value exists (else sec = FLT_MAX: ratio ~ 0)
-        asm volatile("" ::: "memory");
-        int lj = QQ;
-#pragma unroll
-        for (int k4 = QQ - 4; k4 >= 0; k4 -= 4) {
-            float x[4];
-            rd(k4, x);
-#pragma unroll
-            for (int e = 3; e >= 0; --e) lj = x[e] == sec ? k4 + e : lj;
-        }
-        const int si = group_min_i<LPP>(lj < QQ ? d0 + lj : INT_MAX);
-        if (m / sec > uniq && abs(mi - si) > 1) d = Dn + 1;
-    }
-    float f;
-    if (d > Dn - 1) {
-        f = (float)(Dn + 1);
-    } else if (d == 0 || d == Dn - 1) {
-        f = (float)d;
-    } else {
-        const float av = row[d - 1], bv = row[d + 1], cv = row[d];
-        const float xx = d + (av - bv) / (2 * (av + bv - 2 * cv));
-        const float lim = (Dn - 1) * 1.f;
-        f = (lim < xx) ? lim : xx;  // std::min(x, lim)
-    }
-    d_out = d;
-    f_out = f;
-}
-
-template <int V, int PF, int QQ>
-__device__ __forceinline__ void wta_chunk_q(const float (&x)[QQ], const float (*tb)[tbuf_stride<V>()],
-                                            long long pix_top, unsigned pix_off, long long sub_top,
-                                            unsigned sub_off, int cnt, int lane, int Dn, float uniq,
-                                            uint16_t *disp, float *sub) {
-    constexpr int LPP = 64 / PF;  // lanes per pixel
-    static_assert(QQ % 4 == 0 && LPP <= 32, "QQ a multiple of 4, at most 32 lanes per pixel");
-    const int px = lane / LPP, q = lane - px * LPP;
-    const int d0 = q * QQ;
-    const float *row = tb[px < cnt ? px : 0];
-    int d;
-    float f;
-    wta_q_core<LPP, QQ>(x, row, d0, Dn, uniq, d, f);
     if (q == 0 && px < cnt) {
         // disp: only when the frame hands out its raw WTA map (else null:
         // these one-pixel-per-row stores are partial cache lines, ~5% of the

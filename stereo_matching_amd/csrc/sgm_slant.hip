@@ -181,10 +181,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
     using X = SlantExits<UP>;
     constexpr int NX = X::NX;
     __shared__ __attribute__((aligned(16))) SlantLds<V, NW, NE> L;
-    // bottom-up: each compute wave's totals of the last PF steps (its PF
-    // pixels), one padded row each, for the batched WTA (wta_q_core)
-    constexpr int TS = tbuf_stride<V>();
-    __shared__ __attribute__((aligned(16))) float WT[UP ? NW * PF * TS : 4];
     const int wave = wave_id(), lane = tid_x() & 63;
     const int H = g.H, W = g.W, D = g.D;
     const int e0 = lane * V;
@@ -431,25 +427,27 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
         for (int v = 0; v < V; ++v) po[v] = 0.0f;
         float mo = 0.0f;
-        // The WTA + uniqueness + sub-pixel (SGM.cpp:372-418, Solver.cpp:
-        // 569-597) of a wave's pixels runs once per PF steps, for all PF at
-        // once: each step's totals go to the wave's LDS row, and at the last
-        // step of the unrolled group 64/PF lanes take each pixel (wta_q_core,
-        // as the pair final kernel's WTA waves do) -- about a quarter of the
-        // issue cost of one whole-wave WTA per step.  It feeds no chain.
-        auto batch = [&](int sfirst, int cnt) {
-            constexpr int LPP = 64 / PF, QQ = (FULL ? 64 * V : 32) / LPP;
-            static_assert(QQ % 4 == 0, "whole float4 reads per lane");
-            const int px = lane / LPP, qq = lane - px * LPP, d0 = qq * QQ;
-            const float *row = &WT[(k * PF + (px < cnt ? px : 0)) * TS];
+        // the WTA of step s runs in step s + 1, after that step's DP chains
+        // (it feeds no chain): its reductions interleave with theirs instead
+        // of lengthening the step ahead of the barrier.  ptot / pstep: the
+        // deferred step's totals and pixel (pstep < 0: none yet).
+        float ptot[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) ptot[v] = 0.0f;
+        int pstep = -1;
+        auto wta_out = [&](const float (&tt)[V], int ps) {
             int d;
             float f;
-            wta_q_core_lds<LPP, QQ>(row, d0, D, a.uniq, d, f);
-            const int sp = sfirst + px, j = u + sp;
-            if (qq == 0 && px < cnt && j >= 0 && j < W) {
-                const long long pix = (long long)(H - 1 - sp) * W + j;
-                sv.sub[pix] = f;
-                if (sv.disp) sv.disp[pix] = (uint16_t)d;
+            wta_subpixel<V>(tt, D, a.uniq, d, f);
+            // outputs: an inactive step writes the dummy words instead
+            const int j = u + ps;
+            const bool act = ps >= 0 && j >= 0 && j < W;
+            const long long pix = (long long)(H - 1 - ps) * W + j;
+            float *fs = act ? sv.sub + pix : a.dummy + 256;
+            if (lane == 0) *fs = f;
+            if (sv.disp) {
+                uint16_t *ds = act ? sv.disp + pix : reinterpret_cast<uint16_t *>(a.dummy + 257);
+                if (lane == 0) *ds = (uint16_t)d;
             }
         };
         lds_barrier();  // the receiver's prologue phase
@@ -524,7 +522,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     tot[v] = ((rb[1][q][v] + rb[2][q][v]) + L4[v]) + ((rb[3][q][v] + Lo[v]) + L2[v]);
                 store_lds_v<V>(&L.st[cp][k][0][e0], L4);
                 if (lane == 0) L.pm[cp][k][0] = n4;
-                store_lds_v<V>(&WT[(k * PF + q) * TS + e0], tot);
+                wta_out(ptot, pstep);
+#pragma unroll
+                for (int v = 0; v < V; ++v) ptot[v] = tot[v];
+                pstep = s;
             } else {
                 float mm[2] = {lane_min(L2), lane_min(Lo)};
                 wave_min_n<2>(mm);
@@ -542,10 +543,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
             for (int v = 0; v < V; ++v) po[v] = Lo[v];
             mo = no;
-            // (before the refill: this step's ring slot is dead, which
-            // leaves registers for the batch's totals)
-            if constexpr (UP)
-                if (q == PF - 1) batch(s - (PF - 1), PF);  // (q is a constant: no branch)
             refill(q);
 #ifdef SGM_SLANT_STAMPS
             const long long tb0 = __builtin_amdgcn_s_memtime();
@@ -568,8 +565,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
         for (int q = 0; q < PF; ++q)
             if (s0 + q < s_end) step(q, s0 + q);
-        if constexpr (UP)
-            if (s_end > s0) batch(s0, s_end - s0);  // the tile's last partial group
+        if constexpr (UP) wta_out(ptot, pstep);
 #ifdef SGM_SLANT_STAMPS
         if (k == 0 && lane == 0) {
             SLANT_STAMP(0, nsteps);
