@@ -103,6 +103,20 @@ def main():
         d3 = d3[d3 < 1000]
         print(f"    d1 barrier -> exit stores issued {pct(d1)}")
         print(f"    d3 held -> barrier left          {pct(d3)}")
+        # per tile: first and last barrier, steps; tiles in progress over time
+        tb = np.where(have[3], us((br - t0) % (1 << 32)), np.nan)
+        first = np.nanmin(tb, axis=2).ravel()
+        last = np.nanmax(tb, axis=2).ravel()
+        nst = have[3].sum(axis=2).ravel()
+        ok_t = nst > 0
+        first, last, nst = first[ok_t], last[ok_t], nst[ok_t]
+        dur = last - first
+        print(f"    tiles {ok_t.sum()}: steps {pct(nst.astype(float))}".replace(" us", ""))
+        print(f"    tile duration {pct(dur)}; per-step period over a tile {pct(dur / np.maximum(nst - 1, 1))}")
+        span = np.nanmax(last)
+        cuts = np.linspace(0, span, 11)[:-1]
+        act = [int(((first <= c) & (last >= c)).sum()) for c in cuts]
+        print(f"    tiles in progress at 0..90% of the span: {act}")
 
 
 if __name__ == "__main__":
