@@ -618,18 +618,19 @@ int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, i
 //   slant_up (both views): L4, L7, L8 walking up, total
 //     ((S12 + L3) + L4) + ((T56 + L7) + L8), WTA, sub-pixel (row-major maps)
 // the top-down pass's share of the CUs (eighths) while the H pair runs
-// beside it, so that the two finish together: round 5 (the receiver at
-// issue priority, exit states first) moved the best share up at D = 256:
-// HD256 two views 7/8 (12.75 vs 13.09 ms per frame at 4/8), 4K256 two views
-// 6/8 (43.7 vs 44.9; 7/8 44.4): profiles/r05_experiments/r05e_share_*.txt.
-// D = 128 keeps round 4's 6/8 (4K128, HD128: profiles/r04_experiments/slant.txt)
+// beside it, so that the two finish together.  Round 5 (the receiver at
+// issue priority, exit states first) moved the best share up from round 4's
+// 4/8 (D = 256) and 6/8 (D = 128): 7/8 at HD256 two views (12.75 vs 13.09 ms
+// at 4/8), 4K256 one view, HD128 and 4K128 two views; 6/8 only for the
+// largest slanted frames, 4K256 two views (43.7 vs 44.4 at 7/8)
+// (profiles/r05_experiments/r05e_share_*.txt, r05l_share_sizes.txt).
 int slant_down_grid_eighths(Geom g, int nviews) {
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_DOWN_EIGHTHS"))  // share sweeps (tools/slant_share.sh)
         if (atoi(e) >= 1 && atoi(e) <= 8) return atoi(e);
 #endif
-    if (g.D >= 256) return nviews * g.W <= 4096 ? 7 : 6;
-    return 6;
+    const double elems = (double)nviews * g.H * g.W * g.D;
+    return elems > 3e9 ? 6 : 7;
 }
 int slant_cus() {
     int dev = 0, cus = 0;
