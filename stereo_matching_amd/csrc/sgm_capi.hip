@@ -340,8 +340,9 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
 // two views -24%, 720p D = 256 two views -9.4%, HD128 two views -9.6%,
 // 4K128 two views -18.8%; HD256 one view +2.0%, HD128 one view +24.9%,
 // 1056x512 D = 128 two views +10.3%); never at D = 64 (HD64 two views
-// +16.8%, 4K64 +4.2%).  Below that the tile-to-tile hand-off chain, not the
-// bytes, sets the passes' time.
+// +16.8%, 4K64 +4.2%; round 5: +11.4%, +2.2%).  Below that the tile-to-tile
+// hand-off chain, not the bytes, sets the passes' time.  At D = 128 the
+// threshold is 0.9 tiles per workgroup (below).
 bool slant_default(Geom g, int nviews) {
     const double vol = (double)g.W * g.H * g.D * sizeof(float);
     if (vol <= 256.0 * 1024 * 1024 || g.D < 128) return false;
@@ -349,7 +350,11 @@ bool slant_default(Geom g, int nviews) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    return 10LL * nviews * g.W >= 7LL * sgm::kSlantNW * cus;
+    // round 5 re-sweep with the prioritised receiver (profiles/r05_experiments/
+    // r05m_slant_sizes.txt): 720p D = 256 two views (0.71 tiles per
+    // workgroup) -6.2%, but 720p D = 128 two views (0.71) +7.7%: at D = 128
+    // the crossover lies between 0.71 and HD128's 1.07 (-9.6%)
+    return 10LL * nviews * g.W >= (g.D >= 256 ? 7LL : 9LL) * sgm::kSlantNW * cus;
 }
 
 // Rows per band of the backward phase (stage B's diagonal pair, the L8
