@@ -703,6 +703,20 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
     // frame's stream, the pair's wall time; the two launches' own entries
     // overlap in time)
     sa.max_grid = slant_down_grid_eighths(g, nv) * slant_cus() / 8;
+#ifdef SGM_SLANT_DEBUG
+    // timing probes (wrong maps): SGM_SLANT_SOLO=down|hpair runs that launch
+    // alone on all CUs; =seq runs both, one after the other
+    if (const char *solo = getenv("SGM_SLANT_SOLO")) {
+        sa.max_grid = 0;
+        if (strcmp(solo, "hpair") != 0)
+            HIPCHK(h, timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); }));
+        if (strcmp(solo, "down") != 0)
+            HIPCHK(h, timed(h, "stage_a_h", nv * elems, st,
+                            [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, st); }));
+        HIPCHK(h, timed(h, "slant_up", nv * elems, st, [&] { return sgm::launch_slant_up(sa, g, st); }));
+        return SGM_OK;
+    }
+#endif
     HIPCHK(h, timed(h, "slant_down_hpair", nv * elems, st, [&] {
         hipError_t e = hipEventRecord(h->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->st_h, h->ev_fork, 0);
