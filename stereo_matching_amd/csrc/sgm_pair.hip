@@ -155,28 +155,6 @@ __global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, P
     pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, bid_x(), nullptr, nullptr);
 }
 
-// The same H pair with its backward half split over two waves as stage B's
-// H blocks do (pair_split_body: a recompute wave and a backward wave): the
-// row's serial chain is W + W steps instead of W + 2W.  Wave 1 waits for
-// wave 0's forward pass at the workgroup barrier.
-template <int V, bool FULL>
-__global__ __launch_bounds__(128) void hpair2_kernel(PairArgs h1a, PairArgs h2a, PairArgs h1b,
-                                                     PairArgs h2b, Geom g) {
-    constexpr int PFH = V >= 4 ? 16 : 32;
-    constexpr int K = pair_k<V>();
-    __shared__ __attribute__((aligned(16))) SplitLds<K, V> lds;
-    const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
-    const PairArgs h1 = vb ? h1b : h1a;
-    const PairArgs h2 = vb ? h2b : h2a;
-    const int wave = wave_id();
-    if (wave == 0) {
-        pair_fwd_body<0, V, FULL, PFH>(h1, g, bid_x());
-        __threadfence();  // the checkpoint stores, before the backward half reads them
-    }
-    __syncthreads();
-    pair_split_body<PAIR_H, V, FULL, PAIR_INIT2, K, 3>(h2, g, bid_x(), wave, lds, nullptr);
-}
-
 // Stage B blocks are two waves: an H block splits its row's L2 pass into a
 // recompute wave and a backward wave (pair_split_body); a D2 block runs two
 // anti-diagonal L7 chains, one per wave.
@@ -274,13 +252,6 @@ hipError_t launch_stage_a_hpair(const PairArgs *h1, const PairArgs *h2, int nvie
                                 hipStream_t st) {
     const dim3 grid(g.H, nviews);
     const PairArgs &b1 = h1[nviews - 1], &b2 = h2[nviews - 1];
-#ifdef SGM_HPAIR2
-    if (g.D == 32) hpair2_kernel<1, false><<<grid, 128, 0, st>>>(h1[0], h2[0], b1, b2, g);
-    else if (g.D == 64) hpair2_kernel<1, true><<<grid, 128, 0, st>>>(h1[0], h2[0], b1, b2, g);
-    else if (g.D == 128) hpair2_kernel<2, true><<<grid, 128, 0, st>>>(h1[0], h2[0], b1, b2, g);
-    else hpair2_kernel<4, true><<<grid, 128, 0, st>>>(h1[0], h2[0], b1, b2, g);
-    return hipGetLastError();
-#endif
     if (g.D == 32) hpair_kernel<1, false><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);
     else if (g.D == 64) hpair_kernel<1, true><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);
     else if (g.D == 128) hpair_kernel<2, true><<<grid, 64, 0, st>>>(h1[0], h2[0], b1, b2, g);

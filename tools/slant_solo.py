@@ -5,7 +5,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SGM_HIP_LIB"] = os.environ.get("SOLO_LIB") or os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so")
+os.environ["SGM_HIP_LIB"] = os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so")
 os.environ["SGM_SLANT"] = "1"
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
