@@ -779,8 +779,19 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
                                               h->d_ch[0], h->d_ch[1], st);
                }));
         if (vfwd_here) {
-            if ((rc = vfwd_view(h, 1, st)) != SGM_OK) return rc;
-            if ((rc = vfwd_view(h, 0, st)) != SGM_OK) return rc;
+            // both views' vertical passes in one launch: W chains per view
+            // leave the CUs under-filled at KITTI (K64 2 x 69.7 -> 90.7 us,
+            // frame -3.9%; K128 two views 177 -> 166 us)
+            sgm::PairArgs pa[2] = {pair_args(h), pair_args(h)};
+            // (view 1's columns first, view 0's last, as the per-view passes
+            // ran: stage A then finds more of view 0 in the cache, K64 stage
+            // A -3 us, profiles/r05_experiments/r05s_ab_vfwd2.txt)
+            const int v0 = 1, v1 = 0;
+            pa[0].ckpt = h->d_ck[v0][sgm::PAIR_V];
+            pa[1].ckpt = h->d_ck[v1][sgm::PAIR_V];
+            const float *in[2] = {h->d_ch[v0], h->d_ch[v1]};
+            float *out[2] = {cost_buf(h, v0), cost_buf(h, v1)};
+            HIPCHK(h, timed(h, "vfwd", 2.0 * npx * g.D, st, [&] { return sgm::launch_vfwd2(in, out, pa, g, st); }));
         }
     } else {
         if (h->nviews == 2 && (rc = cost_view(h, 1, 1, d_sky_r, sky_pitch, st, vfwd_here)) != SGM_OK)

@@ -106,6 +106,8 @@ hipError_t launch_pair_bwd(int family, int mode, const PairArgs &a, Geom g, hipS
 // both views' vfwd writing C and L3 (the slanted schedule), workgroup y = view
 hipError_t launch_vfwd2_l3(const float *const *in, float *const *out, float *const *l3, const PairArgs *a,
                            Geom g, hipStream_t st);
+// both views' vfwd (C and the L3 checkpoints, a[v].ckpt) in one launch
+hipError_t launch_vfwd2(const float *const *in, float *const *out, const PairArgs *a, Geom g, hipStream_t st);
 // the PAIR_V/PAIR_FINAL pass of two views in one launch
 hipError_t launch_final2(const PairArgs &a0, const PairArgs &a1, Geom g, hipStream_t st);
 // cost_vertical_filter (Solver.cpp:333-368) fused with the L3 forward pass:

@@ -40,16 +40,17 @@ __global__ __launch_bounds__(64) void vfwd_kernel(const float *__restrict__ in,
     vfwd_body<V, FULL, WIN, PF, BAND, L3OUT>(in, out, a, g, bid_x(), tid_x());
 }
 
-// Both views' vertical passes writing C and the whole L3 volume (the slanted
-// schedule) in one launch, workgroup y = view: W chains per view leave about
-// two waves per SIMD at HD, one launch of 2W about four.
-template <int V, bool FULL, int WIN, int PF>
-__global__ __launch_bounds__(64) void vfwd2_l3_kernel(const float *__restrict__ in0, float *__restrict__ out0,
-                                                      PairArgs a0, const float *__restrict__ in1,
-                                                      float *__restrict__ out1, PairArgs a1, Geom g) {
+// Both views' vertical passes in one launch, workgroup y = view: W chains per
+// view leave about one wave per SIMD at KITTI and two at HD, one launch of 2W
+// twice that.  L3OUT: writing C and the whole L3 volume (the slanted
+// schedule), else C and the L3 checkpoints (the joint whole-volume one).
+template <int V, bool FULL, int WIN, int PF, bool L3OUT>
+__global__ __launch_bounds__(64) void vfwd2_kernel(const float *__restrict__ in0, float *__restrict__ out0,
+                                                   PairArgs a0, const float *__restrict__ in1,
+                                                   float *__restrict__ out1, PairArgs a1, Geom g) {
     const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
-    vfwd_body<V, FULL, WIN, PF, false, true>(vb ? in1 : in0, vb ? out1 : out0, vb ? a1 : a0, g, bid_x(),
-                                             tid_x());
+    vfwd_body<V, FULL, WIN, PF, false, L3OUT>(vb ? in1 : in0, vb ? out1 : out0, vb ? a1 : a0, g, bid_x(),
+                                              tid_x());
 }
 
 template <int FD, int V, bool FULL, int PF>
@@ -325,17 +326,19 @@ hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs
     return hipGetLastError();
 }
 
-template <int WIN>
-static void launch_vfwd2_l3_t(const float *const *in, float *const *out, const PairArgs *b, Geom g,
-                              hipStream_t st) {
+template <int WIN, bool L3OUT>
+static void launch_vfwd2_t(const float *const *in, float *const *out, const PairArgs *b, Geom g,
+                           hipStream_t st) {
     const dim3 grid(g.W, 2);
-    if (g.D == 32) vfwd2_l3_kernel<1, false, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
-    else if (g.D == 64) vfwd2_l3_kernel<1, true, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
-    else if (g.D == 128) vfwd2_l3_kernel<2, true, WIN, 16><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+#define VFWD2_ARGS in[0], out[0], b[0], in[1], out[1], b[1], g
+    if (g.D == 32) vfwd2_kernel<1, false, WIN, 16, L3OUT><<<grid, 64, 0, st>>>(VFWD2_ARGS);
+    else if (g.D == 64) vfwd2_kernel<1, true, WIN, 16, L3OUT><<<grid, 64, 0, st>>>(VFWD2_ARGS);
+    else if (g.D == 128) vfwd2_kernel<2, true, WIN, 16, L3OUT><<<grid, 64, 0, st>>>(VFWD2_ARGS);
 #ifndef VFWD2_PF4
 #define VFWD2_PF4 8
 #endif
-    else vfwd2_l3_kernel<4, true, WIN, VFWD2_PF4><<<grid, 64, 0, st>>>(in[0], out[0], b[0], in[1], out[1], b[1], g);
+    else vfwd2_kernel<4, true, WIN, L3OUT ? VFWD2_PF4 : 8, L3OUT><<<grid, 64, 0, st>>>(VFWD2_ARGS);
+#undef VFWD2_ARGS
 }
 
 hipError_t launch_vfwd2_l3(const float *const *in, float *const *out, float *const *l3, const PairArgs *a,
@@ -343,8 +346,14 @@ hipError_t launch_vfwd2_l3(const float *const *in, float *const *out, float *con
     PairArgs b[2] = {a[0], a[1]};
     b[0].out = l3[0];
     b[1].out = l3[1];
-    if (g.scale == 1) launch_vfwd2_l3_t<3>(in, out, b, g, st);
-    else launch_vfwd2_l3_t<1>(in, out, b, g, st);
+    if (g.scale == 1) launch_vfwd2_t<3, true>(in, out, b, g, st);
+    else launch_vfwd2_t<1, true>(in, out, b, g, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_vfwd2(const float *const *in, float *const *out, const PairArgs *a, Geom g, hipStream_t st) {
+    if (g.scale == 1) launch_vfwd2_t<3, false>(in, out, a, g, st);
+    else launch_vfwd2_t<1, false>(in, out, a, g, st);
     return hipGetLastError();
 }
 
