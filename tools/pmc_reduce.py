@@ -19,7 +19,7 @@ NAMES = [("hpair_kernel", "stage_a_h"), ("stage_a_kernel", "stage_a"), ("stage_b
          ("pair_final_kernel", "pair_bwd_L4_final"), ("pair_final2_kernel", "pair_bwd_L4_final"),
          ("vfwd_kernel", "vfwd"), ("cost_h_kernel", "cost_h"), ("cost_h2_kernel", "cost_h"),
          ("cost_h_global_kernel", "cost_h"),
-         ("census_kernel", "census"), ("lr_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc"),
+         ("census_kernel", "census"), ("lr_kernel", "lr"), ("lr_cm_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc"),
          ("sweep_split_kernel<7", "sweep_L8_acc"),
          ("median_fill_kernel", "post_median"), ("cc_local_kernel", "post_cc_local"),
          ("cc_merge_kernel", "post_cc_merge"), ("cc_count_kernel", "post_cc_count"),
@@ -48,8 +48,10 @@ def short(name):
     # the slanted passes, and vfwd writing the whole L3 volume (template L3OUT)
     if "slant_kernel<" in name:
         return "slant_up" if name.split("slant_kernel<")[1].startswith("true") else "slant_down"
-    if "vfwd2_l3_kernel" in name:
-        return "vfwd_l3"
+    # (vfwd2_kernel<V, FULL, WIN, PF, L3OUT>: both views in one launch)
+    if "vfwd2_kernel<" in name:
+        args = name[name.index("vfwd2_kernel<") + len("vfwd2_kernel<"):].split(">")[0].split(", ")
+        return "vfwd_l3" if len(args) >= 5 and args[4] == "true" else "vfwd"
     if "vfwd_kernel<" in name:
         args = name[name.index("vfwd_kernel<") + len("vfwd_kernel<"):].split(">")[0].split(", ")
         if len(args) >= 6 and args[5] == "true":
