@@ -132,7 +132,12 @@ typedef struct sgm_handle sgm_handle;
 int sgm_default_params(sgm_params *p, int h, int w, int s, int d);
 
 /* Allocates every device buffer up front, as the reference constructors do
- * (Solver.cpp:18-27, SGM.cpp:7-24).  device = HIP ordinal. */
+ * (Solver.cpp:18-27, SGM.cpp:7-24).  device = HIP ordinal.  Where the
+ * slanted-tile schedule is chosen by size (HD/4K at D >= 128) and the device
+ * cannot hold its extra buffers (a full L3 volume per view and the hand-off
+ * granules, ~80 GB for a 4K256 pair), the handle takes the banded schedule
+ * instead (the same maps, bit for bit); with SGM_SLANT=1 the allocation
+ * failure is returned. */
 int sgm_create(const sgm_params *p, int device, sgm_handle **out);
 int sgm_destroy(sgm_handle *h);
 const char *sgm_last_error(const sgm_handle *h);

@@ -1080,17 +1080,46 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             for (int f = 0; f < 3 && !rc; ++f)
                 rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D * (f == 2 ? 3 : 1));
         }
+        bool slant_forced = false;
         {
             // the slanted schedule: by size (slant_default), SGM_SLANT=1/0
             // forces it on/off (the parity tests run it at every size)
             const char *e = getenv("SGM_SLANT");
-            const bool want = e && *e ? *e == '1' : slant_default(h->g, h->nviews);
+            slant_forced = e && *e == '1';
+            const bool want = e && *e ? slant_forced : slant_default(h->g, h->nviews);
             h->slant = !p->aux_only && p->solver == SGM_SOLVER_SGM && want;
         }
+        const size_t ng = h->slant ? sgm::slant_gran_count(h->g, h->nviews) : 0;
         if (!rc && h->slant) {
-            for (int v = 0; v < h->nviews && !rc; ++v) rc = dalloc(h, &h->d_l3[v], nvol);
-            const size_t ng = sgm::slant_gran_count(h->g, h->nviews);
-            if (!rc) rc = dalloc(h, &h->d_gran, ng);
+            // its two large buffers: the L3 volumes and the hand-off granules
+            // (~80 GB in all for a 4K256 pair)
+            int arc = SGM_OK;
+            for (int v = 0; v < h->nviews && !arc; ++v) arc = dalloc(h, &h->d_l3[v], nvol);
+            if (!arc) arc = dalloc(h, &h->d_gran, ng);
+#ifdef SGM_SLANT_DEBUG
+            if (!arc && getenv("SGM_SLANT_NO_MEMORY"))  // (tests the fallback below)
+                arc = set_err(h, SGM_ERR_HIP, "hipMalloc: out of memory (forced, SGM_SLANT_NO_MEMORY)");
+#endif
+            if (arc && !slant_forced) {
+                // chosen by size, not asked for: when the device cannot hold
+                // them, the banded schedule (bit-identical maps, no extra
+                // volume) instead of failing sgm_create
+                for (int v = 0; v < 2; ++v) {
+                    if (h->d_l3[v]) h->bytes -= nvol * sizeof(float);
+                    (void)hipFree(h->d_l3[v]);
+                    h->d_l3[v] = nullptr;
+                }
+                if (h->d_gran) h->bytes -= ng * sizeof(unsigned long long);
+                (void)hipFree(h->d_gran);
+                h->d_gran = nullptr;
+                (void)hipGetLastError();  // (the failed hipMalloc's error is not the next launch's)
+                h->err[0] = 0;
+                h->slant = false;
+            } else {
+                rc = arc;
+            }
+        }
+        if (!rc && h->slant) {
             if (!rc) rc = dalloc(h, &h->d_slant_ctl, 2);
             if (!rc) rc = dalloc(h, &h->d_slant_dummy, 512);
             if (!rc && (hipHostMalloc((void **)&h->h_slant_err, sizeof(unsigned), hipHostMallocMapped) != hipSuccess ||

@@ -42,3 +42,52 @@ def test_bench_refuses_invalid_frames():
     assert r.returncode == 3, r.stdout[-2000:] + r.stderr[-3000:]
     assert "the warmup pass produced invalid frames" in r.stderr and "timed out" in r.stderr
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+FALLBACK = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch
+torch.cuda.init()
+from stereo_matching_amd import SGM, SGMError, synthetic
+h, w, D = 240, 1300, 256      # 319 MB per volume, 2 x 1300 columns: slanted by size
+left, right = synthetic.stereo_pair(h, w, D, pair_index=3, kind="road")
+def run():
+    with SGM(h, w, 1, D) as s:
+        s.set_profiling(True)
+        s.process(left, right)
+        s.check()
+        return s.get_lr_disp().copy(), sorted(s.get_profile()), s.device_bytes
+base = run()
+os.environ["SGM_SLANT_NO_MEMORY"] = "1"
+fb = run()
+os.environ["SGM_SLANT"] = "1"
+try:
+    SGM(h, w, 1, D)
+    forced = "created"
+except SGMError as e:
+    forced = str(e)
+print(json.dumps({"base_slant": "slant_up" in base[1], "fb_slant": "slant_up" in fb[1],
+                  "fb_bands": "stage_a_d" in fb[1], "exact": bool(np.array_equal(base[0].view(np.uint32), fb[0].view(np.uint32))),
+                  "bytes": [base[2], fb[2]], "forced": forced}))
+"""
+
+
+@pytest.mark.gpu
+def test_slanted_schedule_falls_back_to_bands_without_memory():
+    # sgm_create (sgm_capi.hip): the slanted schedule's buffers failing to
+    # allocate (forced on the debug build) -> the banded schedule, same maps;
+    # with SGM_SLANT=1 the failure is returned
+    env = {**os.environ, "SGM_HIP_LIB": os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so")}
+    env.pop("SGM_SLANT", None)
+    env.pop("SGM_SLANT_NO_MEMORY", None)
+    r = subprocess.run([sys.executable, "-c", FALLBACK, ROOT], capture_output=True, text=True, timeout=240,
+                       cwd=ROOT, env=env)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads(lines[-1])
+    assert rec["base_slant"] and not rec["fb_slant"] and rec["fb_bands"], rec
+    assert rec["exact"], rec
+    assert rec["bytes"][1] < rec["bytes"][0], rec
+    assert rec["forced"] != "created", rec
+    assert "sgm_create: hipMalloc: out of memory (forced" in r.stderr, r.stderr[-2000:]
