@@ -270,7 +270,7 @@ int sgm_point_cloud_device(sgm_handle *h, const float *d_disp, int pitch, const 
  * thread per device.  RCCL is bound at run time on the first sgm_comm_*
  * call (an RCCL the process already holds, e.g. PyTorch's, is reused;
  * SGM_RCCL_LIB names another).  Errors before a communicator exists are
- * read with sgm_comm_last_error(NULL). */
+ * read with sgm_comm_last_error(NULL), per calling thread (as errno). */
 typedef struct sgm_comm sgm_comm;
 
 #define SGM_COMM_ID_BYTES 128  /* = sizeof(ncclUniqueId) */
@@ -298,7 +298,9 @@ int sgm_comm_info(const sgm_comm *c, int *nranks, int *first_rank, int *nlocal);
  * enqueueing.  Every rank of the communicator must call it with the same
  * rows and cols: from its own host thread, or through sgm_batch_gather_all
  * when one thread drives all ranks.  Call sgm_check on the producing handle
- * first: a map from a frame sgm_check rejects is not valid. */
+ * first: a map from a frame sgm_check rejects is not valid.  A pitched map is
+ * packed into one staging buffer per rank, so one rank's gathers go on one
+ * stream (or are otherwise ordered). */
 int sgm_batch_gather(sgm_comm *c, int rank, const float *d_map, int rows, int cols, int pitch,
                      float *d_root_out, void *stream);
 /* The same for every rank this object holds, from one thread (one RCCL

@@ -56,7 +56,9 @@ struct Rccl {
 
 std::mutex g_mu;
 Rccl g_rccl;
-char g_err[256];  // errors before a communicator exists (sgm_comm_last_error(NULL))
+// errors before a communicator exists (sgm_comm_last_error(NULL)), per
+// calling thread: BatchSGM-style callers create and gather from several
+thread_local char g_err[256];
 
 void set_gerr(const char *fmt, ...) {
     va_list ap;
