@@ -66,3 +66,37 @@ def test_gpus_must_match_world_size():
     assert r.returncode != 0
     assert "--gpus 2 but WORLD_SIZE 1" in r.stderr
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+# kernel families the frame schedules launch (sgm_capi.hip run_frame): every
+# instantiation the library holds must map to a profiler name, so that the PMC
+# passes (tools/pmc_reduce.py) and the timer check see each launch of a frame
+FRAME_KERNELS = ("census_kernel<", "cost_h_kernel<", "cost_h2_kernel<", "cost_h_global_kernel<",
+                 "vfwd_kernel<", "vfwd2_kernel<", "stage_a_kernel<", "stage_a2_kernel<", "stage_b_kernel<",
+                 "stage_b2_kernel<", "hpair_kernel<", "sweep_kernel<7", "sweep2_kernel<7",
+                 "sweep_split_kernel<7", "pair_final_kernel<", "pair_final2_kernel<", "slant_kernel<",
+                 "lr_kernel(", "lr_cm_kernel(", "lk_refine_kernel(", "median_fill_kernel<")
+
+
+def test_pmc_reducer_names_every_frame_kernel():
+    import shutil
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip.so")
+    if not os.path.exists(lib) or not shutil.which("nm"):
+        pytest.skip("library not built or no nm")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_reduce import short
+    out = subprocess.run(["nm", "-C", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    names = {ln.split(" ", 2)[2] for ln in out.splitlines() if ln.count(" ") >= 2 and "_kernel" in ln}
+    seen = set()
+    for fam in FRAME_KERNELS:
+        inst = [n for n in names if "sgm::" + fam in n or "sgm::(anonymous namespace)::" + fam in n]
+        assert inst, f"no {fam} in the library"
+        for n in inst:
+            assert short(n), f"tools/pmc_reduce.py cannot name {n}"
+            seen.add(short(n))
+    # the volume kernels among them carry algorithmic bytes in bench.py
+    for k in ("cost_h", "vfwd", "vfwd_l3", "stage_a", "stage_b", "sweep_L8_acc", "pair_bwd_L4_final",
+              "slant_down", "slant_up", "stage_a_h"):
+        assert k in seen and bench.bytes_per_elem(k, 128) > 0, k
