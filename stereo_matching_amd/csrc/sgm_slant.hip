@@ -174,6 +174,10 @@ struct SlantExits {
 // area -- so hipcc's waitcnt pass keeps exact vmcnt counts and the prefetch
 // rings stay in flight across steps (a branch around a memory instruction
 // makes later waits drain everything outstanding).
+#ifndef SLANT_POLL_GAP
+#define SLANT_POLL_GAP 96
+#endif
+constexpr int kSlantPollGap = SLANT_POLL_GAP;  // sleeps (64 clocks) between the D = 256 re-polls
 template <bool UP, int V, bool FULL, int NW, int PF, int CR>
 __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom g) {
     constexpr int NE = UP ? 2 : 1;         // states exchanged per wave
@@ -279,13 +283,13 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 // decode and check every granule of the slot unconditionally
                 // (bitwise flags): the ring's waits stay exact
                 float y[NX][V];
-                auto decode = [&]() -> bool {
+                auto decode_from = [&](const unsigned long long (&buf)[NX][V]) -> bool {
                     unsigned ok = 1u;
 #pragma unroll
                     for (int x = 0; x < NX; ++x)
 #pragma unroll
                         for (int v = 0; v < V; ++v) {
-                            const unsigned long long q = rq[slot][x][v];
+                            const unsigned long long q = buf[x][v];
                             y[x][v] = granule_value(q);
                             ok &= (unsigned)!need[x] | granule_ok(q, tag);
                         }
@@ -294,6 +298,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #endif
                     return (ok | (unsigned)!dact) != 0u;
                 };
+                auto decode = [&]() -> bool { return decode_from(rq[slot]); };
                 if (!__all(decode())) {
                     // slow path: the next tile is not CR steps ahead
 #ifdef SGM_SLANT_STAMPS
@@ -304,16 +309,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     const unsigned launch_id = id ? id : 1u;
                     dead |= (unsigned)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
                                            &ctl->dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == launch_id);
-                    for (unsigned spins = 1; !dead; ++spins) {
-                        __builtin_amdgcn_s_sleep(1);
-                        // (a compiler barrier: the re-poll loads stay inside the loop)
-                        asm volatile("" ::: "memory");
-#pragma unroll
-                        for (int x = 0; x < NX; ++x) load_granules<V>(rq[slot][x], rrs, (gs * 3 + x) * D * 8 + goff);
-#ifdef SGM_SLANT_STAMPS
-                        nsp = spins;
-#endif
-                        if (__all(decode())) break;
+                    // give-up after the spin limit (the hang guard above)
+                    auto spin_check = [&](unsigned spins) {
                         if (spins >= a.spin_limit) {
                             if (lane == 0) {
                                 atomicAdd(&ctl->err, 1u);
@@ -322,6 +319,55 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                                 __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                             }
                             dead = 1u;
+                        }
+                    };
+                    if constexpr (V >= 4) {
+                        // D = 256: two re-polls in flight, the second issued
+                        // kSlantPollGap sleeps after the first, each re-issued
+                        // as soon as it has been checked.  Polls one after
+                        // the other (each waits its load's full latency before
+                        // the next is issued) hold the states half a loaded
+                        // round trip later on average; with the first
+                        // prefetch one step ahead (CR = 1) this frees the
+                        // registers the second poll needs (HD256 frame
+                        // -3.1%, 4K256 -1%, profiles/r05_experiments/
+                        // r05y_ab_poll*.txt)
+                        unsigned long long qb[NX][V];
+                        auto repoll = [&](unsigned long long (&buf)[NX][V]) {
+                            asm volatile("" ::: "memory");
+#pragma unroll
+                            for (int x = 0; x < NX; ++x) load_granules<V>(buf[x], rrs, (gs * 3 + x) * D * 8 + goff);
+                        };
+                        if (!dead) {
+                            repoll(rq[slot]);
+                            // (s_sleep takes 7 bits: at most 64 x 64 clocks a call)
+#pragma unroll
+                            for (int k = 0; k < kSlantPollGap / 64; ++k) __builtin_amdgcn_s_sleep(64);
+                            if constexpr (kSlantPollGap % 64 != 0) __builtin_amdgcn_s_sleep(kSlantPollGap % 64);
+                            repoll(qb);
+                        }
+                        for (unsigned spins = 1; !dead; ++spins) {
+#ifdef SGM_SLANT_STAMPS
+                            nsp = spins;
+#endif
+                            if (__all(decode())) break;
+                            repoll(rq[slot]);
+                            if (__all(decode_from(qb))) break;
+                            repoll(qb);
+                            spin_check(spins);
+                        }
+                    } else {
+                        for (unsigned spins = 1; !dead; ++spins) {
+                            __builtin_amdgcn_s_sleep(1);
+                            // (a compiler barrier: the re-poll loads stay inside the loop)
+                            asm volatile("" ::: "memory");
+#pragma unroll
+                            for (int x = 0; x < NX; ++x) load_granules<V>(rq[slot][x], rrs, (gs * 3 + x) * D * 8 + goff);
+#ifdef SGM_SLANT_STAMPS
+                            nsp = spins;
+#endif
+                            if (__all(decode())) break;
+                            spin_check(spins);
                         }
                     }
 #ifdef SGM_SLANT_STAMPS
@@ -635,7 +681,7 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
     else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 8><<<grid, block, pad, st>>>(a, g);
     else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 6><<<grid, block, pad, st>>>(a, g);
 #ifndef SLANT_CR4
-#define SLANT_CR4 4
+#define SLANT_CR4 1
 #endif
     else slant_kernel<UP, 4, true, kSlantNW, PF4, SLANT_CR4><<<grid, block, 0, st>>>(a, g);
     return hipGetLastError();
