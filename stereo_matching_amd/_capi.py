@@ -70,15 +70,55 @@ class KernelStat(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("elems", ctypes.c_double)]
 
 
-def build(force: bool = False, jobs: int = 2) -> str:
-    """Compile libsgm_hip.so for gfx950 with hipcc (csrc/Makefile)."""
+# the -DSGM_SLANT_DEBUG build (csrc/Makefile `make dbg`): test infrastructure
+# for the hang-guard tests and the share sweeps, never the product
+DBG_LIB_PATH = os.path.join(_PKG, "libsgm_hip_slantdbg.so")
+
+
+def build(force: bool = False, jobs: int = 2, debug: bool = False) -> str:
+    """Compile libsgm_hip.so for gfx950 with hipcc (csrc/Makefile); debug=True
+    builds the slanted passes' debug library (`make dbg`) instead."""
     if force:
         subprocess.run(["make", "-s", "-C", CSRC, "clean"], check=True)
-    subprocess.run(["make", "-s", "-C", CSRC, f"-j{jobs}"], check=True)
-    return LIB_PATH
+    subprocess.run(["make", "-s", "-C", CSRC, f"-j{jobs}"] + (["dbg"] if debug else []), check=True)
+    return DBG_LIB_PATH if debug else LIB_PATH
 
 
 _lib = None
+
+
+def hip_runtimes() -> list:
+    """The libamdhip64 files mapped into this process (/proc/self/maps)."""
+    found = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split()[-1] if len(line.split()) >= 6 else ""
+                if "libamdhip64.so" in os.path.basename(path) and path not in found:
+                    found.append(path)
+    except OSError:
+        pass
+    return found
+
+
+def _bind_hip_runtime() -> None:
+    """Load PyTorch's HIP runtime before libsgm_hip.so, whatever the caller
+    imported first (INTEGRATION.md "One HIP runtime per process").
+
+    torch's bundled libamdhip64.so and /opt/rocm's libamdhip64.so.7 carry
+    the same soname, so the dynamic loader binds the library's NEEDED entry
+    to whichever copy is already in the process.  With torch loaded first
+    the library and torch share torch's runtime; loaded the other way round,
+    torch's own HIP libraries run beside /opt/rocm's runtime and torch finds
+    no GPU.  Importing torch here (it loads its runtime, it does not
+    initialise a device) makes the order the same for every caller.  Without
+    torch the library binds /opt/rocm's runtime, its RUNPATH."""
+    if os.environ.get("SGM_HIP_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401  (loads torch's libamdhip64.so)
+    except ImportError:
+        return
 
 
 def lib():
@@ -89,7 +129,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise SGMError(SGM_ERR_NO_DEVICE,
                        f"{LIB_PATH} is missing; build it with stereo_matching_amd._capi.build()")
+    _bind_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
+    rts = hip_runtimes()
+    if len(rts) > 1:
+        raise SGMError(SGM_ERR_NO_DEVICE,
+                       "two HIP runtimes are mapped in this process (" + ", ".join(rts) + "): load "
+                       "PyTorch before anything that links /opt/rocm's libamdhip64 "
+                       "(INTEGRATION.md \"One HIP runtime per process\")")
     P = ctypes.c_void_p
     I = ctypes.c_int
     PP = ctypes.POINTER(Params)

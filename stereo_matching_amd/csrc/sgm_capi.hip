@@ -717,14 +717,20 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
         return SGM_OK;
     }
 #endif
+    bool hpair_first = false;
+#ifdef SGM_SLANT_DEBUG
+    hpair_first = getenv("SGM_SLANT_HPAIR_FIRST") != nullptr;  // launch-order probe
+#endif
     HIPCHK(h, timed(h, "slant_down_hpair", nv * elems, st, [&] {
         hipError_t e = hipEventRecord(h->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->st_h, h->ev_fork, 0);
-        if (e == hipSuccess)
-            e = timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); });
-        if (e == hipSuccess)
-            e = timed(h, "stage_a_h", nv * elems, h->st_h,
-                      [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, h->st_h); });
+        auto down = [&] { return timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); }); };
+        auto hpair = [&] {
+            return timed(h, "stage_a_h", nv * elems, h->st_h,
+                         [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, h->st_h); });
+        };
+        if (e == hipSuccess) e = hpair_first ? hpair() : down();
+        if (e == hipSuccess) e = hpair_first ? down() : hpair();
         if (e == hipSuccess) e = hipEventRecord(h->ev_join, h->st_h);
         if (e == hipSuccess) e = hipStreamWaitEvent(st, h->ev_join, 0);
         return e;
@@ -1080,6 +1086,33 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             for (int f = 0; f < 3 && !rc; ++f)
                 rc = dalloc(h, &h->d_carry[v][f], (size_t)h->g.W * h->g.D * (f == 2 ? 3 : 1));
         }
+        h->band_rows = band_rows_for(h->g);
+        if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
+            for (int v = 0; v < 2 && !rc; ++v) {
+                if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
+                rc = dalloc(h, &h->d_sub[v], npx);
+            }
+        } else if (!rc && h->nviews == 1) {  // stage_lr needs a second sub-pixel map
+            rc = dalloc(h, &h->d_sub[1], npx);
+        }
+        if (!rc) rc = dalloc(h, &h->d_cloud_counts, (size_t)h->g.H + 1);
+        if (!rc) rc = dalloc(h, &h->d_out, npx);
+        if (!rc) rc = dalloc(h, &h->d_min, npx);
+        if (!rc) rc = dalloc(h, &h->d_zero, 256);
+        if (!rc) rc = dalloc(h, &h->d_pf_orig, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_work, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_label, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_count, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_area, npx);
+        if (!rc) rc = dalloc(h, &h->d_pf_snap, sgm::post_snapshot_floats(h->g));
+        if (!rc) rc = dalloc(h, &h->d_lk_in, npx);
+        if (!rc) rc = dalloc(h, &h->d_sky_scratch, 2 * sgm::sky_scratch_bytes(h->g));
+        if (!rc) rc = dalloc(h, &h->d_pf_changes, (size_t)kMedianMaxLaunches);
+        if (!rc && hipHostMalloc((void **)&h->h_pf_changes, sizeof(int), hipHostMallocDefault) !=
+                       hipSuccess)
+            rc = set_err(h, SGM_ERR_HIP, "hipHostMalloc of the post-filter counter failed");
+        if (!rc && hipMemset(h->d_zero, 0, 256 * sizeof(float)) != hipSuccess)
+            rc = set_err(h, SGM_ERR_HIP, "hipMemset of the zero page failed");
         bool slant_forced = false;
         {
             // the slanted schedule: by size (slant_default), SGM_SLANT=1/0
@@ -1092,7 +1125,9 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
         const size_t ng = h->slant ? sgm::slant_gran_count(h->g, h->nviews) : 0;
         if (!rc && h->slant) {
             // its two large buffers: the L3 volumes and the hand-off granules
-            // (~80 GB in all for a 4K256 pair)
+            // (about 28 GB for a 4K256 pair, whose whole handle is about 80 GB:
+            // INTEGRATION.md 5), allocated after every common buffer, so that
+            // the fallback below covers any shortage they cause
             int arc = SGM_OK;
             for (int v = 0; v < h->nviews && !arc; ++v) arc = dalloc(h, &h->d_l3[v], nvol);
             if (!arc) arc = dalloc(h, &h->d_gran, ng);
@@ -1134,33 +1169,6 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
                         hipMemset(h->d_slant_ctl, 0, 2 * sizeof(sgm::SlantCtl)) != hipSuccess))
                 rc = set_err(h, SGM_ERR_HIP, "hipMemset of the slanted schedule's hand-off state failed");
         }
-        h->band_rows = band_rows_for(h->g);
-        if (!rc && p->aux_only) {  // the side stages' maps (stage_lr, the raw map copy)
-            for (int v = 0; v < 2 && !rc; ++v) {
-                if ((rc = dalloc(h, &h->d_disp[v], npx))) break;
-                rc = dalloc(h, &h->d_sub[v], npx);
-            }
-        } else if (!rc && h->nviews == 1) {  // stage_lr needs a second sub-pixel map
-            rc = dalloc(h, &h->d_sub[1], npx);
-        }
-        if (!rc) rc = dalloc(h, &h->d_cloud_counts, (size_t)h->g.H + 1);
-        if (!rc) rc = dalloc(h, &h->d_out, npx);
-        if (!rc) rc = dalloc(h, &h->d_min, npx);
-        if (!rc) rc = dalloc(h, &h->d_zero, 256);
-        if (!rc) rc = dalloc(h, &h->d_pf_orig, npx);
-        if (!rc) rc = dalloc(h, &h->d_pf_work, npx);
-        if (!rc) rc = dalloc(h, &h->d_pf_label, npx);
-        if (!rc) rc = dalloc(h, &h->d_pf_count, npx);
-        if (!rc) rc = dalloc(h, &h->d_pf_area, npx);
-        if (!rc) rc = dalloc(h, &h->d_pf_snap, sgm::post_snapshot_floats(h->g));
-        if (!rc) rc = dalloc(h, &h->d_lk_in, npx);
-        if (!rc) rc = dalloc(h, &h->d_sky_scratch, 2 * sgm::sky_scratch_bytes(h->g));
-        if (!rc) rc = dalloc(h, &h->d_pf_changes, (size_t)kMedianMaxLaunches);
-        if (!rc && hipHostMalloc((void **)&h->h_pf_changes, sizeof(int), hipHostMallocDefault) !=
-                       hipSuccess)
-            rc = set_err(h, SGM_ERR_HIP, "hipHostMalloc of the post-filter counter failed");
-        if (!rc && hipMemset(h->d_zero, 0, 256 * sizeof(float)) != hipSuccess)
-            rc = set_err(h, SGM_ERR_HIP, "hipMemset of the zero page failed");
     } while (0);
     if (rc) {
         fprintf(stderr, "sgm_create: %s\n", h->err[0] ? h->err : "HIP stream/event creation failed");
@@ -1202,8 +1210,9 @@ void *sgm_get_stream(const sgm_handle *h) { return h ? (void *)h->st : nullptr; 
 // are wrong.  It sets a host-mapped word; the next call on the handle (or
 // sgm_process, after its own frame) reports it and clears it.
 int check_slant_err(sgm_handle *h) {
-    if (!h->h_slant_err || !*(volatile unsigned *)h->h_slant_err) return SGM_OK;
-    *(volatile unsigned *)h->h_slant_err = 0;
+    // read and clear in one step: a give-up stored by a frame still running
+    // between a plain read and a plain clear would be lost
+    if (!h->h_slant_err || !__atomic_exchange_n(h->h_slant_err, 0u, __ATOMIC_ACQ_REL)) return SGM_OK;
     return set_err(h, SGM_ERR_HIP, "slanted aggregation: a tile hand-off timed out; that frame's maps are invalid");
 }
 
@@ -1214,7 +1223,8 @@ int sgm_check(sgm_handle *h) {
     // ev_last; on the handle's own stream, that stream (the H pair's stream
     // is joined into the frame's stream before the bottom-up pass)
     if (h->last_st && h->last_recorded) HIPCHK(h, hipEventSynchronize(h->ev_last));
-    else HIPCHK(h, hipStreamSynchronize(h->st));
+    else if (!h->last_st || h->last_st == h->st) HIPCHK(h, hipStreamSynchronize(h->st));
+    else HIPCHK(h, hipDeviceSynchronize());  // a caller's stream whose end could not be recorded
     return check_slant_err(h);
 }
 

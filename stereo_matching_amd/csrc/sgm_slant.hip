@@ -40,14 +40,18 @@
 
 namespace sgm {
 
-// Per-step LDS exchange of one tile: the exchanged chain states (NE per wave:
-// bottom-up L4 and L8, top-down L6) and their minima, for the previous step
-// (parity (s-1)&1) and this one (s&1); slots NW and NW+1 hold the next tile's
-// wave 0 / wave 1 states, put there by the receiver wave.
-template <int V, int NW, int NE>
+// LDS exchange of one tile: the exchanged chain states (NE per wave:
+// bottom-up L4 and L8, top-down L6) and their minima in a ring of R steps
+// (step s in slot s & (R-1)); slots NW and NW+1 hold the next tile's wave 0 /
+// wave 1 states, put there by the receiver wave.  No workgroup barrier per
+// step: done[w + 2] is the last step whose states wave w (0..NW-1) has
+// published, done[NW + 2] = done[NW + 3] the receiver's; done[0], done[1]
+// stand for waves -2 and -1, which consume nothing (DESIGN.md 5e "Dataflow").
+template <int V, int NW, int NE, int R>
 struct SlantLds {
-    float st[2][NW + 2][NE][64 * V];
-    float pm[2][NW + 2][NE];
+    float st[R][NW + 2][NE][64 * V];
+    float pm[R][NW + 2][NE];
+    int done[NW + 4];
     int ticket;
     unsigned epoch;
 };
@@ -166,7 +170,7 @@ struct SlantExits {
 };
 
 // PF: steps of data loads in flight per compute wave; CR: phases of hand-off
-// granule loads in flight in the receiver.
+// granule loads in flight in the receiver; R: steps in the LDS state ring.
 //
 // Memory-instruction hygiene (as the other passes): every
 // load and store of the steady-state loops is unconditional -- load
@@ -174,17 +178,63 @@ struct SlantExits {
 // area -- so hipcc's waitcnt pass keeps exact vmcnt counts and the prefetch
 // rings stay in flight across steps (a branch around a memory instruction
 // makes later waits drain everything outstanding).
+//
+// Dataflow inside a tile (DESIGN.md 5e "Dataflow"): a compute wave's step s
+// waits only for the states it reads -- wave k+1's (bottom-up) and k+2's of
+// step s-1 -- and for the waves that read its own ring slot (k-1 bottom-up,
+// k-2) to be past step s-R; the receiver waits only for waves NW-1 and NW-2.
+// Waves 0 and 1, which produce the exit states, depend on the next tile's
+// states of about 7 steps before (the k+2 family), so they run ahead of the
+// receiver's hop instead of meeting it at a barrier every step.
 #ifndef SLANT_POLL_GAP
 #define SLANT_POLL_GAP 96
 #endif
 constexpr int kSlantPollGap = SLANT_POLL_GAP;  // sleeps (64 clocks) between the D = 256 re-polls
-template <bool UP, int V, bool FULL, int NW, int PF, int CR>
+#ifndef SLANT_PUB_WAIT
+#define SLANT_PUB_WAIT 1
+#endif
+
+// a step counter's wait: done[ia] and done[ib] >= thr_ab, done[ic] and
+// done[id] >= thr_cd (wave-uniform indices and thresholds; INT_MIN: no
+// condition).  Spins with a bounded count; returns false when it gave up (the
+// caller reports it: the hang guard).
+__device__ __forceinline__ int lds_word(const int *p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ bool flow_wait(const int *done, int ia, int ib, int thr_ab, int ic, int id,
+                                          int thr_cd, unsigned limit) {
+    for (unsigned spins = 0;; ++spins) {
+        const int va = lds_word(done + ia), vb = lds_word(done + ib);
+        const int vc = lds_word(done + ic), vd = lds_word(done + id);
+        if (min(va, vb) >= thr_ab && min(vc, vd) >= thr_cd) break;
+        if (spins >= limit) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    // (the state reads that follow stay below the counter reads)
+    asm volatile("" ::: "memory");
+    return true;
+}
+
+// publish step s as done[idx] (lanes 0..n-1 store idx .. idx+n-1): after this
+// wave's LDS stores of the step (LDS executes a wave's DS instructions in
+// order; SLANT_PUB_WAIT also waits for their completion first)
+__device__ __forceinline__ void flow_publish(int *done, int idx, int n, int s, int lane) {
+#if SLANT_PUB_WAIT
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the prefetch ring stays in flight
+#endif
+    asm volatile("" ::: "memory");
+    if (lane < n) __hip_atomic_store(done + idx + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+}
+
+template <bool UP, int V, bool FULL, int NW, int PF, int CR, int R>
 __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom g) {
     constexpr int NE = UP ? 2 : 1;         // states exchanged per wave
     constexpr int K2 = UP ? 1 : 0;         // index of the wave k+2 family (L8 / L6)
+    static_assert(R >= 2 && (R & (R - 1)) == 0, "ring of a power of two steps");
     using X = SlantExits<UP>;
     constexpr int NX = X::NX;
-    __shared__ __attribute__((aligned(16))) SlantLds<V, NW, NE> L;
+    __shared__ __attribute__((aligned(16))) SlantLds<V, NW, NE, R> L;
     const int wave = wave_id(), lane = tid_x() & 63;
     const int H = g.H, W = g.W, D = g.D;
     const int e0 = lane * V;
@@ -204,12 +254,28 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
     if (tid_x() == 0)
         L.epoch = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float p2v = to_vgpr(a.p2);
+    // an LDS wait never waits for anything outside the workgroup but the
+    // receiver, whose polls are bounded (and which publishes after giving
+    // up): this limit, far above the receiver's, only turns a bug into a
+    // reported error instead of a hang
+    const unsigned flow_limit = a.spin_limit > (0xffffffffu >> 8) ? 0xffffffffu : a.spin_limit << 8;
     // hang guard (receiver wave): once a poll of this launch gave up -- this
     // wave's, or any workgroup's (ctl->dead == this launch's id) -- later
     // polls skip their wait, so a neighbour that never stores costs one spin
     // limit per launch, not one per step (the frame's maps are invalid
     // anyway, and the host reports it: sgm_capi.hip check_slant_err)
     unsigned dead = 0;
+    auto give_up = [&]() {
+        const unsigned id = __builtin_amdgcn_readfirstlane(L.epoch) + 1u;
+        const unsigned launch_id = id ? id : 1u;
+        if (lane == 0) {
+            atomicAdd(&ctl->err, 1u);
+            atomicExch(&ctl->dead, launch_id);
+            // (the host reports it: sgm_capi.hip check_slant_err)
+            __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        dead = 1u;
+    };
 
     for (;;) {
         __syncthreads();
@@ -228,25 +294,31 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         const int s_begin = max(0, -(u_lo + NW - 1));
         const int s_end = min(H, W - u_lo);
         const int nsteps = s_end - s_begin;
+        // the tile's counters: every compute wave "published" step s_begin-1
+        // (never read by an active pixel: a path start zeroes it, and the only
+        // active pixel of a step s_begin > 0 is wave NW-1's, which reads the
+        // receiver's slots); the receiver's prologue phase publishes s_begin-1
+        if (wave == 0 && lane < NW + 4)
+            L.done[lane] = lane < 2 ? INT_MAX : (lane < NW + 2 ? s_begin - 1 : s_begin - 2);
+        __syncthreads();
 #ifdef SGM_SLANT_DEBUG
         const unsigned stall = (unsigned)(UP && view == 0 && t == a.stall_tile);
 #endif
 
         if (wave == NW) {
             // ----------------------------------------------- receiver wave
-            // the receiver's phase ends every step of the tile: issue
+            // the receiver's phases feed the tile's last two waves: issue
             // priority over the compute waves (HD256 slant_up -7%, 4K256
             // -4..7%: profiles/r05_experiments/r05d_ab_*.txt)
 #ifndef SLANT_RECV_PRIO
 #define SLANT_RECV_PRIO 3
 #endif
             __builtin_amdgcn_s_setprio(SLANT_RECV_PRIO);
-            // Phase p = 0 .. nsteps (the prologue, then one per step; each
-            // ends on the tile's barrier) hands the next tile's exit states
-            // of step gs = s_begin - 1 + p to LDS parity gs & 1 (slots NW,
-            // NW+1), which step gs + 1 reads.  Their granule loads run CR
-            // phases ahead; a phase re-polls only when the next tile is not
-            // that far ahead.
+            // Phase p = 0 .. nsteps (the prologue, then one per step) hands
+            // the next tile's exit states of step gs = s_begin - 1 + p to ring
+            // slot gs & (R-1) (slots NW, NW+1), which waves NW-1 and NW-2 read
+            // in their step gs + 1.  Their granule loads run CR phases ahead;
+            // a phase re-polls only when the next tile is not that far ahead.
             auto gvalid = [&](int p) {
                 return t + 1 < T && (p >= 1 || s_begin >= 1) && p < nsteps;
             };
@@ -263,6 +335,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             };
 #pragma unroll
             for (int q = 0; q < CR; ++q) issue(q, q);
+            // ring reuse: waves NW-2 and NW-1 (done[NW], done[NW+1]) read the
+            // slot a phase overwrites
 #ifdef SGM_SLANT_STAMPS
             long long rw = 0, rb = 0, rt = __builtin_amdgcn_s_memtime();
             long long rp_phases = 0, rp_polls = 0, rp_ticks = 0;  // added once per tile
@@ -305,21 +379,15 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                     const long long sp0 = __builtin_amdgcn_s_memtime();
                     unsigned nsp = 0;
 #endif
-                    const unsigned id = __builtin_amdgcn_readfirstlane(L.epoch) + 1u;
-                    const unsigned launch_id = id ? id : 1u;
-                    dead |= (unsigned)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                           &ctl->dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == launch_id);
+                    {
+                        const unsigned id = __builtin_amdgcn_readfirstlane(L.epoch) + 1u;
+                        const unsigned launch_id = id ? id : 1u;
+                        dead |= (unsigned)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                               &ctl->dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == launch_id);
+                    }
                     // give-up after the spin limit (the hang guard above)
                     auto spin_check = [&](unsigned spins) {
-                        if (spins >= a.spin_limit) {
-                            if (lane == 0) {
-                                atomicAdd(&ctl->err, 1u);
-                                atomicExch(&ctl->dead, launch_id);
-                                // (the host reports it: sgm_capi.hip check_slant_err)
-                                __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            }
-                            dead = 1u;
-                        }
+                        if (spins >= a.spin_limit) give_up();
                     };
                     if constexpr (V >= 4) {
                         // D = 256: two re-polls in flight, the second issued
@@ -380,11 +448,20 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 if (lane == 0 && want) hop_mark(UP, 2, T, H, view, t, gs);
 #endif
                 // (a phase with nothing wanted writes slots that no valid
-                // predecessor reads)
-                const int par = gs & 1;
+                // successor reads)
+                const int par = gs & (R - 1);
+#ifdef SGM_SLANT_STAMPS
+                const long long t0_ = __builtin_amdgcn_s_memtime();
+                rw += t0_ - rt;
+#endif
+                if (!flow_wait(L.done, NW, NW + 1, gs - R + 1, NW, NW + 1, INT_MIN, flow_limit)) give_up();
+#ifdef SGM_SLANT_STAMPS
+                rt = __builtin_amdgcn_s_memtime();
+                rb += rt - t0_;
+#endif
                 // the states to LDS, then their minima, all NX reductions
-                // interleaved (this phase ends the tile's step: it sits on
-                // the tile-to-tile hop)
+                // interleaved (this phase sits on the tile-to-tile hop,
+                // DESIGN.md 5e)
                 float mx[NX];
 #pragma unroll
                 for (int x = 0; x < NX; ++x) {
@@ -399,16 +476,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
 #pragma unroll
                     for (int x = 0; x < NX; ++x) L.pm[par][NW + X::wave(x)][X::kind(x)] = mx[x];
                 }
+                flow_publish(L.done, NW + 2, 2, gs, lane);
                 issue(slot, p + CR);
-#ifdef SGM_SLANT_STAMPS
-                const long long t0_ = __builtin_amdgcn_s_memtime();
-                rw += t0_ - rt;
-                lds_barrier();
-                rt = __builtin_amdgcn_s_memtime();
-                rb += rt - t0_;
-#else
-                lds_barrier();
-#endif
             };
             const int np = nsteps + 1;
             int p0 = 0;
@@ -454,6 +523,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             const int sc = uniform(min(max(s, s_lo), s_hi));
             return never ? (long long)e0 : base + (long long)sc * dstep;
         };
+        // the step counters this wave waits on (done[w + 2] is wave w's): its
+        // producers k+1 (bottom-up L4) and k+2 need step s-1, its ring slot's
+        // readers k-1 (bottom-up) and k-2 step s-R+1 (top-down: k+2 and k-2
+        // only, each index given twice)
+        const int i_p1 = UP ? k + 3 : k + 4, i_r1 = UP ? k + 1 : k;
         constexpr int NS = UP ? 4 : 1;  // streams: C (+ S12, L3, T56)
         float rb[NS][PF][V];
         int pfs = s_begin;  // step of the next ring refill
@@ -474,9 +548,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         for (int v = 0; v < V; ++v) po[v] = 0.0f;
         float mo = 0.0f;
         // the WTA of step s runs in step s + 1, after that step's DP chains
-        // (it feeds no chain): its reductions interleave with theirs instead
-        // of lengthening the step ahead of the barrier.  ptot / pstep: the
-        // deferred step's totals and pixel (pstep < 0: none yet).
+        // and its publish (it feeds no chain).  ptot / pstep: the deferred
+        // step's totals and pixel (pstep < 0: none yet).
         float ptot[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) ptot[v] = 0.0f;
@@ -496,7 +569,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 if (lane == 0) *ds = (uint16_t)d;
             }
         };
-        lds_barrier();  // the receiver's prologue phase
 #ifdef SGM_SLANT_STAMPS
         long long st_prev = __builtin_amdgcn_s_memtime(), st_work = 0, st_wait = 0;
         const long long tile_t0 = st_prev;
@@ -505,7 +577,16 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         auto step = [&](int q, int s) {
             const int j = u + s;
             const bool act = j >= 0 && j < W;
-            const int pp = (s - 1) & 1, cp = s & 1;
+            const int pp = (s - 1) & (R - 1), cp = s & (R - 1);
+#ifdef SGM_SLANT_STAMPS
+            const long long tw0 = __builtin_amdgcn_s_memtime();
+            st_work += tw0 - st_prev;
+#endif
+            if (!flow_wait(L.done, i_p1, k + 4, s - 1, i_r1, k, s - R + 1, flow_limit)) give_up();
+#ifdef SGM_SLANT_STAMPS
+            st_prev = __builtin_amdgcn_s_memtime();
+            st_wait += st_prev - tw0;
+#endif
             // path starts (SGM.cpp:93-98, :165-170, :205-214, :259-276,
             // :321-335): a zero state before the first pixel makes the step
             // yield L = C (P1, P2 >= 0)
@@ -554,20 +635,24 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             for (int v = 0; v < V; ++v) zo[v] = vo ? po[v] : 0.0f;
             const float mmo = vo ? mo : 0.0f;
             dp_step<V>(zo, mmo, c, Lo, a.p1, p2v);
-            float no, n2;
+            float no;
             if constexpr (UP) {
                 float mm[3] = {lane_min(L4), lane_min(L2), lane_min(Lo)};
                 wave_min_n<3>(mm);
-                const float n4 = mm[0];
-                n2 = mm[1];
                 no = mm[2];
+                // the exchanged states out first: the waves below wait for them
+                store_lds_v<V>(&L.st[cp][k][0][e0], L4);
+                store_lds_v<V>(&L.st[cp][k][K2][e0], L2);
+                if (lane == 0) {
+                    L.pm[cp][k][0] = mm[0];
+                    L.pm[cp][k][K2] = mm[1];
+                }
+                flow_publish(L.done, k + 2, 1, s, lane);
                 // ((S12 + L3) + L4) + ((T56 + L7) + L8)
                 float tot[V];
 #pragma unroll
                 for (int v = 0; v < V; ++v)
                     tot[v] = ((rb[1][q][v] + rb[2][q][v]) + L4[v]) + ((rb[3][q][v] + Lo[v]) + L2[v]);
-                store_lds_v<V>(&L.st[cp][k][0][e0], L4);
-                if (lane == 0) L.pm[cp][k][0] = n4;
                 wta_out(ptot, pstep);
 #pragma unroll
                 for (int v = 0; v < V; ++v) ptot[v] = tot[v];
@@ -575,8 +660,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
             } else {
                 float mm[2] = {lane_min(L2), lane_min(Lo)};
                 wave_min_n<2>(mm);
-                n2 = mm[0];
                 no = mm[1];
+                store_lds_v<V>(&L.st[cp][k][K2][e0], L2);
+                if (lane == 0) L.pm[cp][k][K2] = mm[0];
+                flow_publish(L.done, k + 2, 1, s, lane);
                 // T56 = L5 + L6 (streamed: the bottom-up pass reads it once)
                 float o[V];
 #pragma unroll
@@ -584,24 +671,13 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
                 float *dst = act ? sv.t56w + off_of(s) : a.dummy + e0;
                 store_v_nt<V>(dst, o, dact);
             }
-            store_lds_v<V>(&L.st[cp][k][K2][e0], L2);
-            if (lane == 0) L.pm[cp][k][K2] = n2;
+#ifdef SGM_SLANT_HOPS
+            if (k == 0 && lane == 0) hop_mark(UP, 3, T, H, view, t, s);
+#endif
 #pragma unroll
             for (int v = 0; v < V; ++v) po[v] = Lo[v];
             mo = no;
             refill(q);
-#ifdef SGM_SLANT_STAMPS
-            const long long tb0 = __builtin_amdgcn_s_memtime();
-            st_work += tb0 - st_prev;
-#endif
-            lds_barrier();
-#ifdef SGM_SLANT_STAMPS
-            st_prev = __builtin_amdgcn_s_memtime();
-            st_wait += st_prev - tb0;
-#endif
-#ifdef SGM_SLANT_HOPS
-            if (k == 0 && lane == 0) hop_mark(UP, 3, T, H, view, t, s);
-#endif
         };
         int s0 = s_begin;
         for (; s0 + PF <= s_end; s0 += PF) {
@@ -677,13 +753,19 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_LDSPAD")) pad = (size_t)atoi(e) * 1024;
 #endif
-    if (g.D == 32) slant_kernel<UP, 1, false, kSlantNW, PF, 8><<<grid, block, pad, st>>>(a, g);
-    else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 8><<<grid, block, pad, st>>>(a, g);
-    else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 6><<<grid, block, pad, st>>>(a, g);
+    // R: the LDS state ring (steps a wave may run ahead of the waves that
+    // read its states); D = 256 bottom-up: 4 x 32 KB
+#ifndef SLANT_RING
+#define SLANT_RING 4
+#endif
+    constexpr int R = SLANT_RING;
+    if (g.D == 32) slant_kernel<UP, 1, false, kSlantNW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 6, R><<<grid, block, pad, st>>>(a, g);
 #ifndef SLANT_CR4
 #define SLANT_CR4 1
 #endif
-    else slant_kernel<UP, 4, true, kSlantNW, PF4, SLANT_CR4><<<grid, block, 0, st>>>(a, g);
+    else slant_kernel<UP, 4, true, kSlantNW, PF4, SLANT_CR4, R><<<grid, block, 0, st>>>(a, g);
     return hipGetLastError();
 }
 

@@ -22,11 +22,11 @@ def oracle_lib():
 
 
 def pytest_sessionstart(session):
-    # GPU sessions: initialise PyTorch's HIP runtime before anything loads
-    # libsgm_hip.so.  The process then holds two HIP runtimes (PyTorch's
-    # bundled one and /opt/rocm's, which the library links); PyTorch's finds
-    # no GPU when the other initialised first, so the tests that use torch
-    # device tensors depend on this order, as bench.py does.
+    # GPU sessions: initialise PyTorch's HIP runtime up front.  The library
+    # shares it (torch's libamdhip64.so and /opt/rocm's have one soname, and
+    # _capi.lib() imports torch before it loads libsgm_hip.so: INTEGRATION.md
+    # "One HIP runtime per process"); this only makes the device
+    # initialisation happen once, before the first test.
     expr = session.config.getoption("markexpr", "") or ""
     if "gpu" in expr and "not gpu" not in expr:
         try:

@@ -51,6 +51,29 @@ int main(int argc, char **argv) {
         } catch (const std::runtime_error &e) {
             std::printf("BatchSGM threw: %s\n", e.what());
         }
+        // BatchSGM's round bookkeeping and argument checks (no device work):
+        // 2N+1 pairs on N devices are rounds of N, N and 1
+        using B = sgm_amd::BatchSGM;
+        bad += B::round_count(9, 0, 4) != 4 || B::round_count(9, 4, 4) != 4 || B::round_count(9, 8, 4) != 1;
+        bad += B::round_count(3, 0, 1) != 1 || B::round_count(3, 2, 1) != 1 || B::round_count(8, 0, 8) != 8;
+        {
+            std::vector<Mat> l2(2, Mat(6, 8, CV_8UC1)), r1(1, Mat(6, 8, CV_8UC1)), r2(2, Mat(6, 8, CV_8UC1));
+            std::vector<Mat> wrong(2, Mat(6, 9, CV_8UC1)), f32(2, Mat(6, 8, CV_32FC1));
+            const struct {
+                const std::vector<Mat> &l, &r;
+                const char *why;
+            } cases[] = {{l2, r1, "counts differ"}, {l2, wrong, "constructed size"}, {f32, r2, "CV_8UC1"}};
+            for (const auto &c : cases) {
+                try {
+                    B::check_batch(c.l, c.r, 6, 8);
+                    std::printf("check_batch accepted a bad batch (%s)\n", c.why);
+                    ++bad;
+                } catch (const std::runtime_error &e) {
+                    std::printf("check_batch threw: %s\n", e.what());
+                }
+            }
+            B::check_batch(l2, r2, 6, 8);  // a valid batch passes
+        }
         Mat m(4, 5, CV_32FC1);
         m.at<float>(3, 4) = 2.5f;
         Mat shallow = m;

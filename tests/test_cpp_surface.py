@@ -47,6 +47,7 @@ def test_header_compiles_and_asserts(exe):
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("threw as expected") == 4
     assert "BatchSGM threw" in r.stdout
+    assert r.stdout.count("check_batch threw") == 3
 
 
 @pytest.mark.gpu
@@ -180,14 +181,17 @@ def test_class_surface_one_sided_sky_masks(exe, tmp_path, masks):
 
 
 @pytest.mark.gpu
-def test_batch_sgm_matches_oracle(exe, tmp_path):
+@pytest.mark.parametrize("n", [3, 5])
+def test_batch_sgm_matches_oracle(exe, tmp_path, n):
     # include/sgm_amd/BatchSGM.h: SGM(h, w, s, d) per device, one host thread
     # per device, sgm_check, then sgm_batch_gather_all (ncclGather) to the
-    # first device; on a one-GPU box 3 pairs run in 3 rounds of 1.  Every
-    # get_disp(k) equals the oracle's post-filtered map for pair k.
+    # first device; on a one-GPU box 2N+1 = 3 (and 5) pairs run in rounds of
+    # 1, so the double-buffered maps, root buffers and host staging each
+    # cycle, and each round's gather and copy-out overlap the next round's
+    # frame.  Every get_disp(k) equals the oracle's post-filtered map for pair k.
     import oracle
     oracle.build()
-    h, w, D, n = 72, 200, 64, 3
+    h, w, D = 72, 200, 64
     prefix = str(tmp_path / "pair")
     want = []
     for k in range(n):
@@ -200,7 +204,7 @@ def test_batch_sgm_matches_oracle(exe, tmp_path):
                        capture_output=True, text=True, timeout=120,
                        env={**os.environ, "SGM_AMD_DEVICES": "0"})
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "batch of 3 pairs on 1 device(s)" in r.stdout
+    assert f"batch of {n} pairs on 1 device(s)" in r.stdout
     got = np.fromfile(fo, dtype=np.float32).reshape(n, h, w)
     for k in range(n):
         assert np.array_equal(got[k].view(np.uint32), want[k].view(np.uint32)), k

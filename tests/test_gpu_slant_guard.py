@@ -11,11 +11,25 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DBG = os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def dbg_lib():
+    # the debug library is built with the release one (__graft_entry__.build,
+    # `make dbg`); a tree built with plain `make` gets it here
+    if not os.path.exists(DBG):
+        from stereo_matching_amd import _capi
+        _capi.build(debug=True)
+    return DBG
 
 
 @pytest.mark.gpu
-def test_slant_guard_and_small_grids():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "slant_guard.py")],
+@pytest.mark.parametrize("D", [64, 256])
+def test_slant_guard_and_small_grids(D):
+    # D = 256 runs the receiver's other give-up loop (two re-polls in flight,
+    # sgm_slant.hip V >= 4) and the four-step LDS ring at its largest
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "slant_guard.py"), "--D", str(D)],
                        capture_output=True, text=True, timeout=180, cwd=ROOT)
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert lines, r.stdout[-2000:] + r.stderr[-3000:]
@@ -24,6 +38,8 @@ def test_slant_guard_and_small_grids():
     st = rec["stall"]
     assert st["code"] == 3 and "timed out" in st["message"], st
     assert st["frame_s"] < 20, st          # bounded: one spin limit, not one per step
+    # the release build's limit (2^22 polls) gives up within a minute
+    assert 0 < st["release_give_up_s"] < 60, st
     assert rec["recovery"] == {"exact": True, "check_ok": True}
     assert all(v["exact"] for v in rec["grids"].values()), rec["grids"]
     assert r.returncode == 0
@@ -34,7 +50,7 @@ def test_bench_refuses_invalid_frames():
     # bench.py checks every pass's frames (sgm_check) before it reports a
     # time: with a forced hand-off stall (debug build, slanted schedule
     # forced on the K128 frame) it prints no JSON line and exits 3
-    env = {**os.environ, "SGM_HIP_LIB": os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so"),
+    env = {**os.environ, "SGM_HIP_LIB": DBG,
            "SGM_SLANT": "1", "SGM_SLANT_STALL": "20", "SGM_SLANT_SPIN_LIMIT": "2000"}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
                         "--no-cpu-baseline", "--no-profile-pass"],
@@ -78,7 +94,7 @@ def test_slanted_schedule_falls_back_to_bands_without_memory():
     # sgm_create (sgm_capi.hip): the slanted schedule's buffers failing to
     # allocate (forced on the debug build) -> the banded schedule, same maps;
     # with SGM_SLANT=1 the failure is returned
-    env = {**os.environ, "SGM_HIP_LIB": os.path.join(ROOT, "stereo_matching_amd", "libsgm_hip_slantdbg.so")}
+    env = {**os.environ, "SGM_HIP_LIB": DBG}
     env.pop("SGM_SLANT", None)
     env.pop("SGM_SLANT_NO_MEMORY", None)
     r = subprocess.run([sys.executable, "-c", FALLBACK, ROOT], capture_output=True, text=True, timeout=240,

@@ -16,7 +16,9 @@ schedule (SGM_SLANT=1), and prints one JSON line:
   * grids: SGM_SLANT_GRID = 1, 2, 3 workgroups per pass (tiles claimed in the
     order T-1 .. 0, so a tile's producer always holds a workgroup or has
     finished) give bit-exact maps: the deadlock-freedom argument of
-    sgm_slant.hip at the smallest grids.
+    sgm_slant.hip at the smallest grids;
+  * the give-up's cost per poll (the stall at ten times the spin limit) and
+    the release build's give-up time it extrapolates to (kSlantSpinLimit).
 
 Usage (GPU): python tools/slant_guard.py [--h 64 --w 200 --D 64]
 """
@@ -80,6 +82,7 @@ def main():
         os.environ["SGM_SLANT_STALL"] = str(ntiles // 2)
         t0 = time.perf_counter()
         m = frame()
+        torch.cuda.synchronize(dev)
         err = None
         try:
             sgm.check()
@@ -90,6 +93,21 @@ def main():
                         "code": None if err is None else err.code,
                         "message": None if err is None else str(err),
                         "maps_differ": not exact(m)}
+        # the give-up's cost per poll: the same stall at ten times the spin
+        # limit; the slope extrapolates to the release build's kSlantSpinLimit
+        os.environ["SGM_SLANT_SPIN_LIMIT"] = str(10 * args.spin_limit)
+        t0 = time.perf_counter()
+        frame()
+        torch.cuda.synchronize(dev)
+        t10 = time.perf_counter() - t0
+        try:
+            sgm.check()
+        except SGMError:
+            pass
+        per_spin = max(t10 - out["stall"]["frame_s"], 0.0) / (9 * args.spin_limit)
+        out["stall"]["frame_s_10x"] = round(t10, 4)
+        out["stall"]["us_per_spin"] = round(per_spin * 1e6, 3)
+        out["stall"]["release_give_up_s"] = round(per_spin * (1 << 22), 2)  # kSlantSpinLimit
         del os.environ["SGM_SLANT_STALL"], os.environ["SGM_SLANT_SPIN_LIMIT"]
         # 2. the next frame is valid again
         m = frame()

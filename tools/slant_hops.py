@@ -1,6 +1,10 @@
-"""Hop timeline of the slanted passes: when each tile's
-exit states were stored, when the next tile's receiver needed and held them,
-and when each step's barrier was left (s_memrealtime, 100 MHz, chip-wide).
+"""Hop timeline of the slanted passes: when
+each tile's exit states were stored, when the next tile's receiver needed and
+held them, and when compute wave 0 published each step (s_memrealtime,
+100 MHz, chip-wide).  Round 6's passes have no per-step barrier (DESIGN.md 5e
+"Dataflow"): "lead" is how long before the consumer's phase began the
+producer had issued the states it needs -- positive when the exits were
+produced ahead of their consumer.
 
 Library built with -DSGM_SLANT_HOPS (bash tools/variant.sh hops
 -DSGM_SLANT_HOPS), loaded with SGM_HIP_LIB=build/hops/libsgm_hip.so.
@@ -11,10 +15,11 @@ Printed per pass:
     holding the states, over the phases in which the receiver had to wait
     (held - needed > 0.2 us) and over all phases;
   * wait: held - needed, the time the receiver's phase waited for the hop;
-  * step: barrier(t, s) - barrier(t, s-1), the tile's step period, split by
-    whether the step's input hop made the receiver wait;
-  * lag: barrier(t, s) - barrier(t+1, s-1), how far a tile runs behind its
-    producer."""
+  * lead: needed(t, s) - stored(t+1, s), the producer's head start;
+  * step: published(t, s) - published(t, s-1), wave 0's step period, split
+    by whether the step's input hop made the receiver wait;
+  * lag: published(t, s) - published(t+1, s-1), how far a tile runs behind
+    its producer."""
 import ctypes
 import os
 import sys
@@ -80,7 +85,12 @@ def main():
         print(f"    hop  (waited) {pct(hop[waited])}")
         print(f"    hop  (all)    {pct(hop)}")
         print(f"    wait (waited) {pct(wait[waited])}")
-        # step periods: barrier(t, s) - barrier(t, s-1); the input of step s is
+        lead = us((nd[:, :-1, :] - st[:, 1:, :]) % (1 << 32))
+        lead = np.where(lead > 2 ** 31 / 100, lead - 2 ** 32 / 100, lead)[ok]
+        print(f"    lead (consumer needs - producer stored) {pct(lead)}; "
+              f"exits stored before the consumer needed them in {(lead > 0).mean() * 100:.1f}%, "
+              f"more than 2 us before in {(lead > 2).mean() * 100:.1f}%")
+        # step periods: published(t, s) - published(t, s-1); the input of step s is
         # the hand-off of step s-1 (phase gs = s-1)
         okb = have[3][:, :, 1:] & have[3][:, :, :-1]
         per = us((br[:, :, 1:] - br[:, :, :-1]) % (1 << 32))
@@ -94,15 +104,10 @@ def main():
         lag = us((br[:, :-1, 1:] - br[:, 1:, :-1]) % (1 << 32))
         lag = np.where(lag > 2 ** 31 / 100, lag - 2 ** 32 / 100, lag)
         print(f"    lag behind the producer tile {pct(lag[okl])}")
-        # the hop loop: producer barrier(t+1, s-1) -> its exit-state stores
-        # (d1) -> consumer holds them (hop) -> consumer barrier(t, s) (d3)
+        # producer wave 0: its step s-1 published -> its step s exit stores (d1)
         okd = have[0][:, :, 1:] & have[3][:, :, :-1]
         d1 = us((st[:, :, 1:] - br[:, :, :-1]) % (1 << 32))[okd]
-        okh = have[2] & have[3]
-        d3 = us((br - hd) % (1 << 32))[okh]
-        d3 = d3[d3 < 1000]
-        print(f"    d1 barrier -> exit stores issued {pct(d1)}")
-        print(f"    d3 held -> barrier left          {pct(d3)}")
+        print(f"    d1 published(s-1) -> exit stores of s issued {pct(d1)}")
         # per tile: first and last barrier, steps; tiles in progress over time
         tb = np.where(have[3], us((br - t0) % (1 << 32)), np.nan)
         first = np.nanmin(tb, axis=2).ravel()
