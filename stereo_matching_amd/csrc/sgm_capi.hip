@@ -335,8 +335,9 @@ hipError_t pair_bwd(sgm_handle *h, int fam, int mode, const sgm::PairArgs &a, hi
 // The slanted-tile schedule replaces the bands (above the Infinity Cache)
 // where it was measured faster (tools/slant_sizes.py,
 // profiles/r04_experiments/slant.txt, with the H pair beside the top-down
-// pass): at D >= 128 once views * W >= 0.7 * NW * CUs, i.e. 0.7 full-height
-// tiles of work per workgroup (HD256 two views -18.6%, 4K256 one view -20%,
+// pass): at D = 256 once views * W >= 0.5 * NW * CUs, i.e. half a full-height
+// tile of work per workgroup (round 6; 0.7 before), at D = 128 from 0.9
+// (round 4 at 0.7: HD256 two views -18.6%, 4K256 one view -20%,
 // two views -24%, 720p D = 256 two views -9.4%, HD128 two views -9.6%,
 // 4K128 two views -18.8%; HD256 one view +2.0%, HD128 one view +24.9%,
 // 1056x512 D = 128 two views +10.3%); never at D = 64 (HD64 two views
@@ -353,8 +354,12 @@ bool slant_default(Geom g, int nviews) {
     // round 5 re-sweep with the prioritised receiver (profiles/r05_experiments/
     // r05m_slant_sizes.txt): 720p D = 256 two views (0.71 tiles per
     // workgroup) -6.2%, but 720p D = 128 two views (0.71) +7.7%: at D = 128
-    // the crossover lies between 0.71 and HD128's 1.07 (-9.6%)
-    return 10LL * nviews * g.W >= (g.D >= 256 ? 7LL : 9LL) * sgm::kSlantNW * cus;
+    // the crossover lies between 0.71 and HD128's 1.07 (-9.6%).  Round 6's
+    // dataflow passes (profiles/r06_experiments/r06c_sizes_sweep.txt,
+    // r06f_share_order_sweep.txt) moved D = 256 down: HD256 one view (0.54)
+    // -5.0..-9.7%; at D = 128, 720p two views (0.71) stays +5.3%, HD128 one
+    // view (0.54) +24%
+    return 10LL * nviews * g.W >= (g.D >= 256 ? 5LL : 9LL) * sgm::kSlantNW * cus;
 }
 
 // Rows per band of the backward phase (stage B's diagonal pair, the L8
@@ -623,19 +628,20 @@ int finish_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, i
 //   slant_up (both views): L4, L7, L8 walking up, total
 //     ((S12 + L3) + L4) + ((T56 + L7) + L8), WTA, sub-pixel (row-major maps)
 // the top-down pass's share of the CUs (eighths) while the H pair runs
-// beside it, so that the two finish together.  Round 5 (the receiver at
-// issue priority, exit states first) moved the best share up from round 4's
-// 4/8 (D = 256) and 6/8 (D = 128): 7/8 at HD256 two views (12.75 vs 13.09 ms
-// at 4/8), 4K256 one view, HD128 and 4K128 two views; 6/8 only for the
-// largest slanted frames, 4K256 two views (43.7 vs 44.4 at 7/8)
-// (profiles/r05_experiments/r05e_share_*.txt, r05l_share_sizes.txt).
+// beside it.  Round 6 (dataflow passes, profiles/r06_experiments/
+// r06f_share_order_sweep.txt, best of 3): the top-down pass alone now takes
+// 1.9 ms at HD256 (it took the whole 4.7 ms region before), so the share
+// that balances the two moved: 4/8 for D = 256 frames below 2e9 elements
+// (HD256 V=2 10.83 ms vs 11.12 at 8/8, HD256 V=1, 720p256 V=2), the whole
+// chip otherwise (4K256 V=1/V=2, HD128 and 4K128 V=2 within 0.5% of their
+// best at 8/8).  Launching the H pair first was no better at any share.
 int slant_down_grid_eighths(Geom g, int nviews) {
 #ifdef SGM_SLANT_DEBUG
     if (const char *e = getenv("SGM_SLANT_DOWN_EIGHTHS"))  // share sweeps (tools/slant_share.sh)
         if (atoi(e) >= 1 && atoi(e) <= 8) return atoi(e);
 #endif
     const double elems = (double)nviews * g.H * g.W * g.D;
-    return elems > 3e9 ? 6 : 7;
+    return g.D >= 256 && elems < 2e9 ? 4 : 8;
 }
 int slant_cus() {
     int dev = 0, cus = 0;
@@ -717,20 +723,14 @@ int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
         return SGM_OK;
     }
 #endif
-    bool hpair_first = false;
-#ifdef SGM_SLANT_DEBUG
-    hpair_first = getenv("SGM_SLANT_HPAIR_FIRST") != nullptr;  // launch-order probe
-#endif
     HIPCHK(h, timed(h, "slant_down_hpair", nv * elems, st, [&] {
         hipError_t e = hipEventRecord(h->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->st_h, h->ev_fork, 0);
-        auto down = [&] { return timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); }); };
-        auto hpair = [&] {
-            return timed(h, "stage_a_h", nv * elems, h->st_h,
-                         [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, h->st_h); });
-        };
-        if (e == hipSuccess) e = hpair_first ? hpair() : down();
-        if (e == hipSuccess) e = hpair_first ? down() : hpair();
+        if (e == hipSuccess)
+            e = timed(h, "slant_down", nv * elems, st, [&] { return sgm::launch_slant_down(sa, g, st); });
+        if (e == hipSuccess)
+            e = timed(h, "stage_a_h", nv * elems, h->st_h,
+                      [&] { return sgm::launch_stage_a_hpair(hp1, hp2, nv, g, h->st_h); });
         if (e == hipSuccess) e = hipEventRecord(h->ev_join, h->st_h);
         if (e == hipSuccess) e = hipStreamWaitEvent(st, h->ev_join, 0);
         return e;

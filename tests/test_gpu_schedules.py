@@ -131,16 +131,17 @@ def test_calls_on_different_streams_are_ordered():
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("views", [2, 1])
 def test_slant_default_by_size(views, monkeypatch):
-    # sgm_capi.hip slant_default: at D >= 128 above the Infinity Cache the
-    # slanted passes run once every workgroup gets 0.7 full-height tiles of
-    # work (views x W >= 0.7 x 14 x CUs; on a 256-CU MI355X HD256 with two
-    # views, 3840 >= 2508.8, without one view, 1920), else the bands.  The
-    # expectation uses the device's own CU count, as the library does.
+    # sgm_capi.hip slant_default: at D = 256 above the Infinity Cache the
+    # slanted passes run once every workgroup gets 0.5 full-height tiles of
+    # work (views x W >= 0.5 x 14 x CUs; on a 256-CU MI355X HD256 with two
+    # views, 3840 >= 1792, and with one view, 1920: both slanted since round
+    # 6's dataflow passes), else the bands.  The expectation uses the
+    # device's own CU count, as the library does.
     import torch
     monkeypatch.delenv("SGM_SLANT", raising=False)
     h, w, D = 1080, 1920, 256
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    slanted = 10 * views * w >= 7 * 14 * cus
+    slanted = 10 * views * w >= 5 * 14 * cus
     left, right = synthetic.stereo_pair(h, w, D, pair_index=0)
     with SGM(h, w, 1, D, views=views) as sgm:
         sgm.set_profiling(True)

@@ -28,16 +28,10 @@ for (h, w, D, V) in sizes:
     dl, dr = torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev)
     out = torch.empty((h, w), dtype=torch.float32, device=dev)
     variants = [("base", "0", None)] + [(f"slant{e}", "1", str(e)) for e in eighths]
-    if os.environ.get("HFIRST"):  # the H pair launched first, at each share
-        variants += [(f"hfirst{e}", "1", str(e)) for e in eighths]
     res = {}
     for rep in range(REPS):
         for name, sl, e in variants:
             os.environ["SGM_SLANT"] = sl
-            if name.startswith("hfirst"):
-                os.environ["SGM_SLANT_HPAIR_FIRST"] = "1"
-            else:
-                os.environ.pop("SGM_SLANT_HPAIR_FIRST", None)
             if e is None:
                 os.environ.pop("SGM_SLANT_DOWN_EIGHTHS", None)
             else:
