@@ -141,7 +141,13 @@ hipError_t launch_vfwd_l3(const float *in, float *out, float *l3, const PairArgs
 // Compute waves per tile; one more wave per workgroup, the receiver, turns
 // the next tile's exit-state granules into LDS states (the compute waves 0
 // and 1 store this tile's own exit states themselves).
-constexpr int kSlantNW = 14;
+// The bottom-up pass's tiles are 15 columns wide (16 waves, the workgroup
+// maximum): its hand-off granules cost 3 / NW of a tile-step's bytes, and
+// slant_up ran 3.9-4.0% faster at HD256 with 15 than with 14; the top-down
+// pass keeps 14 (with 15 the H pair beside it lost more than it gained,
+// profiles/r06_experiments/r06l_tile_width.txt).
+constexpr int kSlantNW = 14;     // top-down
+constexpr int kSlantNWUp = 15;   // bottom-up
 // Polls before a receiver gives up on a hand-off (a hang guard: seconds).
 constexpr unsigned kSlantSpinLimit = 1u << 22;
 // Launch bookkeeping of one slanted pass kind, in device memory (zeroed at
@@ -176,7 +182,7 @@ struct SlantArgs {
                           // receiver of this tile of view 0 never accepts a granule, to
                           // exercise the give-up path; -1: none
 };
-size_t slant_tiles(Geom g);
+size_t slant_tiles(Geom g, int nw);
 // granules (8 B each) of nviews views' hand-offs
 size_t slant_gran_count(Geom g, int nviews);
 // both views' (a.nviews) bottom-up slanted pass: L4 + L7 + L8 + WTA (ctl[1])

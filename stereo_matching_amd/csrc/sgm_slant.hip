@@ -714,16 +714,18 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
     }
 }
 
-size_t slant_tiles(Geom g) { return (size_t)((g.W + g.H - 1 + kSlantNW - 1) / kSlantNW); }
+size_t slant_tiles(Geom g, int nw) { return (size_t)((g.W + g.H - 1 + nw - 1) / nw); }
 
 size_t slant_gran_count(Geom g, int nviews) {
-    return (size_t)nviews * slant_tiles(g) * g.H * 3 * g.D;
+    // (both passes share the buffer: the narrower tiles' count)
+    return (size_t)nviews * slant_tiles(g, kSlantNW < kSlantNWUp ? kSlantNW : kSlantNWUp) * g.H * 3 * g.D;
 }
 
 template <bool UP>
 static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
     SlantArgs a = a0;
-    a.ntiles = (int)slant_tiles(g);
+    constexpr int NW = UP ? kSlantNWUp : kSlantNW;
+    a.ntiles = (int)slant_tiles(g, NW);
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -738,7 +740,7 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
     if (const char *e = getenv("SGM_SLANT_SPIN_LIMIT")) a.spin_limit = atoi(e) > 0 ? (unsigned)atoi(e) : a.spin_limit;
     if (const char *e = getenv("SGM_SLANT_STALL")) a.stall_tile = *e ? atoi(e) : -1;
 #endif
-    const dim3 grid(a.grid), block(64 * (kSlantNW + 1));
+    const dim3 grid(a.grid), block(64 * (NW + 1));
 #ifndef SLANT_PF_UP4
 #define SLANT_PF_UP4 4
 #endif
@@ -759,13 +761,13 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
 #define SLANT_RING 4
 #endif
     constexpr int R = SLANT_RING;
-    if (g.D == 32) slant_kernel<UP, 1, false, kSlantNW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
-    else if (g.D == 64) slant_kernel<UP, 1, true, kSlantNW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
-    else if (g.D == 128) slant_kernel<UP, 2, true, kSlantNW, PF, 6, R><<<grid, block, pad, st>>>(a, g);
+    if (g.D == 32) slant_kernel<UP, 1, false, NW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 64) slant_kernel<UP, 1, true, NW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
+    else if (g.D == 128) slant_kernel<UP, 2, true, NW, PF, 6, R><<<grid, block, pad, st>>>(a, g);
 #ifndef SLANT_CR4
 #define SLANT_CR4 1
 #endif
-    else slant_kernel<UP, 4, true, kSlantNW, PF4, SLANT_CR4, R><<<grid, block, 0, st>>>(a, g);
+    else slant_kernel<UP, 4, true, NW, PF4, SLANT_CR4, R><<<grid, block, 0, st>>>(a, g);
     return hipGetLastError();
 }
 

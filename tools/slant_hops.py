@@ -32,7 +32,7 @@ import torch  # noqa: E402
 
 from stereo_matching_amd import SGM, _capi, synthetic  # noqa: E402
 
-NW = 14
+NW, NW_UP = 14, 15  # tile widths: top-down, bottom-up (sgm_internal.h)
 
 
 def pct(x):
@@ -52,8 +52,8 @@ def main():
     sgm = SGM(h, w, 1, D, views=V, device=0)
     lib = _capi.lib()
     lib.sgm_debug_slant_hops.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    T = (w + h - 1 + NW - 1) // NW
-    n = V * T * h
+    TS = {0: (w + h - 1 + NW - 1) // NW, 1: (w + h - 1 + NW_UP - 1) // NW_UP}  # per pass
+    n = V * max(TS.values()) * h
     for _ in range(3):
         sgm.process_device(dl.data_ptr(), dr.data_ptr(), out.data_ptr())
     sgm.check()
@@ -64,10 +64,11 @@ def main():
     prof = sgm.get_profile()
     buf = np.zeros((2, 4, n), np.uint32)
     assert lib.sgm_debug_slant_hops(buf.ctypes.data, n, 0) == 0
-    print(f"{w}x{h} D={D} V={V}: {T} tiles per view; slant_down {prof['slant_down'][1]:.3f} ms, "
+    print(f"{w}x{h} D={D} V={V}: {TS[0]} / {TS[1]} tiles per view (top-down / bottom-up); slant_down {prof['slant_down'][1]:.3f} ms, "
           f"slant_up {prof['slant_up'][1]:.3f} ms")
     for p, name in ((0, "top-down"), (1, "bottom-up")):
-        a = buf[p].reshape(4, V, T, h).astype(np.int64)
+        T = TS[p]
+        a = buf[p][:, :V * T * h].reshape(4, V, T, h).astype(np.int64)
         have = a != 0
         t0 = a[have].min()
 
