@@ -756,11 +756,16 @@ static hipError_t launch_slant_t(const SlantArgs &a0, Geom g, hipStream_t st) {
     if (const char *e = getenv("SGM_SLANT_LDSPAD")) pad = (size_t)atoi(e) * 1024;
 #endif
     // R: the LDS state ring (steps a wave may run ahead of the waves that
-    // read its states); D = 256 bottom-up: 4 x 32 KB
-#ifndef SLANT_RING
-#define SLANT_RING 4
+    // read its states): 2 bottom-up, 4 top-down (HD256 paired: R = 2 for both
+    // made slant_up 2.4% faster and the top-down pass beside the H pair 6%
+    // slower; profiles/r06_experiments/r06n_knobs_ab.txt)
+#ifndef SLANT_RING_UP
+#define SLANT_RING_UP 2
 #endif
-    constexpr int R = SLANT_RING;
+#ifndef SLANT_RING_DN
+#define SLANT_RING_DN 4
+#endif
+    constexpr int R = UP ? SLANT_RING_UP : SLANT_RING_DN;
     if (g.D == 32) slant_kernel<UP, 1, false, NW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
     else if (g.D == 64) slant_kernel<UP, 1, true, NW, PF, 8, R><<<grid, block, pad, st>>>(a, g);
     else if (g.D == 128) slant_kernel<UP, 2, true, NW, PF, 6, R><<<grid, block, pad, st>>>(a, g);

@@ -6,6 +6,11 @@
 set -o pipefail
 CFG=$1; REPS=$2; shift 2
 mkdir -p gpurun_out
+# one discarded run first: a fresh box runs its first seconds measurably
+# faster than later ones (profiles/r06_experiments/r06l_tile_width.txt), which
+# would favour whichever library ran first
+SGM_HIP_LIB=$1 timeout -k 10 120 python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline \
+  > /dev/null 2>> gpurun_out/ab.err || { echo "warm-up bench failed"; tail -20 gpurun_out/ab.err; exit 1; }
 for r in $(seq 1 $REPS); do
   for L in "$@"; do
     SGM_HIP_LIB=$L timeout -k 10 120 python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline \
