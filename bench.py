@@ -88,12 +88,13 @@ def bytes_per_elem(name: str, D: int) -> float:
         "stage_a_h": (4.0 + ck) + (8.0 + ck),
         # the slanted-tile schedule (DESIGN.md "Slanted tiles"): vfwd writing
         # the whole L3 volume; the top-down pass reads C and writes T56; the
-        # bottom-up pass reads C, S12, L3 and T56.  Each tile of NW = 14
-        # columns also hands 2 (top-down) or 3 (bottom-up) D-vectors per step
-        # to the next tile as 8-byte granules, written once and read once
+        # bottom-up pass reads C, S12, L3 and T56.  Each tile (NW = 14 columns
+        # top-down, 15 bottom-up) also hands 2 (top-down) or 3 (bottom-up)
+        # D-vectors per step to the next tile as 8-byte granules, written
+        # once and read once
         "vfwd_l3": 12.0,
         "slant_down": 8.0 + 2 * 16.0 / 14,
-        "slant_up": 16.0 + 3 * 16.0 / 14,
+        "slant_up": 16.0 + 3 * 16.0 / 15,
     }
     # the top-down pass and the H pair run concurrently (two streams); the
     # library also times the pair as one region, fork to join
