@@ -151,9 +151,6 @@ __global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, P
     const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
     const PairArgs h1 = vb ? h1b : h1a;
     const PairArgs h2 = vb ? h2b : h2a;
-#ifdef SGM_HPAIR_PRIO
-    __builtin_amdgcn_s_setprio(SGM_HPAIR_PRIO);
-#endif
     pair_fwd_body<0, V, FULL, PFH>(h1, g, bid_x());
     __threadfence();  // this wave's checkpoint stores, before it reads them back
     pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, bid_x(), nullptr, nullptr);
