@@ -93,6 +93,11 @@ def bytes_per_elem(name: str, D: int) -> float:
         # D-vectors per step to the next tile as 8-byte granules, written
         # once and read once
         "vfwd_l3": 12.0,
+        # its cost stage as checkpoints + strips (sgm_vstrip.hip):
+        # the horizontal IIR's state (3 floats) at every 16-column strip edge,
+        # written by cost_ck and read by vstrip, which writes C and L3
+        "cost_ck": 3 * 4.0 / 16,
+        "vstrip": 3 * 4.0 / 16 + 8.0,
         "slant_down": 8.0 + 2 * 16.0 / 14,
         "slant_up": 16.0 + 3 * 16.0 / 15,
     }

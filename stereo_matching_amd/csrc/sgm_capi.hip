@@ -53,6 +53,7 @@ struct sgm_handle {
     float *d_ck[2][3];    // checkpoints per view and pair family (H, V, D2)
     float *d_carry[2][3]; // banded backward passes: chain state at band edges (L7, L8, L4)
     bool slant;           // the slanted-tile schedule (sgm_slant.hip, DESIGN.md "Slanted tiles")
+    bool vstrip;          //   its cost stage as checkpoints + strips (sgm_vstrip.hip; SGM_VSTRIP=0: off)
     float *d_l3[2];       // slant: the full L3 volume per view
     unsigned long long *d_gran;  // slant: hand-off granules (both views)
     sgm::SlantCtl *d_slant_ctl;  // slant: launch bookkeeping of the passes
@@ -651,13 +652,15 @@ int slant_cus() {
     return cus;
 }
 
-int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st) {
+// have_c: the strip pass already wrote C and the L3 volumes (run_frame)
+int slant_views(sgm_handle *h, float *sub0, uint16_t *raw, hipStream_t st, bool have_c) {
     const Geom g = h->g;
     const int nv = h->nviews;
     const double elems = (double)g.H * g.W * g.D;
     sgm::PairArgs hp1[2], hp2[2];
     sgm::SlantArgs sa{};
-    if (nv == 2) {  // both views in one launch
+    if (have_c) {
+    } else if (nv == 2) {  // both views in one launch
         const sgm::PairArgs pa[2] = {pair_args(h), pair_args(h)};
         const float *in[2] = {h->d_ch[0], h->d_ch[1]};
         float *out[2] = {h->d_c[0], h->d_c[1]}, *l3[2] = {h->d_l3[0], h->d_l3[1]};
@@ -779,7 +782,38 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // slanted schedule runs its own vertical pass
     const bool banded = h->band_rows > 0;
     const bool vfwd_here = !banded && !h->slant;
-    if (both_h) {
+    // the slanted schedule's cost stage as checkpoints + strips (sgm_vstrip.hip):
+    // C and the L3 volumes in one pass, 9 B per element instead of cost_h's
+    // 4 and vfwd_l3's 12
+    const uint8_t *sky0 = right_only ? d_sky_r : d_sky_l;
+    const bool vstrip = h->slant && h->vstrip && sgm::vstrip_supported(g, sky0 != nullptr) &&
+                        (h->nviews == 1 || (sky0 == nullptr) == (d_sky_r == nullptr));
+    if (vstrip) {
+        const int dsi0 = right_only ? 1 : 0;
+        HIPCHK(h, timed(h, "cost_ck", h->nviews * npx * g.D, st, [&] {
+                   return sgm::launch_cost_ck(h->d_ct[0], h->d_ct[1], sky0, d_sky_r, sky_pitch, dsi0, 1,
+                                              h->nviews, g, h->d_ch[0], h->d_ch[1], st);
+               }));
+        sgm::VStripArgs va{};
+        va.ctl = h->d_ct[0];
+        va.ctr = h->d_ct[1];
+        va.sky0 = sky0;
+        va.sky1 = d_sky_r;
+        va.sky_pitch = sky_pitch;
+        va.dsi0 = dsi0;
+        va.dsi1 = 1;
+        va.ck0 = h->d_ch[0];  // (the checkpoints sit in the dead Ch volumes)
+        va.ck1 = h->d_ch[1];
+        va.c0 = h->d_c[0];
+        va.c1 = h->d_c[1];
+        va.l30 = h->d_l3[0];
+        va.l31 = h->d_l3[1];
+        va.dummy = h->d_slant_dummy;
+        va.p1 = (float)h->p.p1;
+        va.p2 = (float)h->p.p2;
+        HIPCHK(h, timed(h, "vstrip", h->nviews * npx * g.D, st,
+                        [&] { return sgm::launch_vstrip(va, h->nviews, g, st); }));
+    } else if (both_h) {
         HIPCHK(h, timed(h, "cost_h", 2.0 * npx * g.D, st, [&] {
                    return sgm::launch_cost_h2(h->d_ct[0], h->d_ct[1], d_sky_l, d_sky_r, sky_pitch, g,
                                               h->d_ch[0], h->d_ch[1], st);
@@ -815,7 +849,7 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     // pass writes row-major ones
     const bool cm = h->nviews == 2 && !h->slant;
     if (h->slant) {
-        if ((rc = slant_views(h, sub0, d_raw, st)) != SGM_OK) return rc;
+        if ((rc = slant_views(h, sub0, d_raw, st, vstrip)) != SGM_OK) return rc;
     } else if (h->nviews == 2 && !banded && 2.0 * vol_bytes <= 256.0 * 1024 * 1024) {
         // both volumes fit the Infinity Cache together: joint launches
         if ((rc = aggregate_joint(h, sub0, d_raw, 1, st)) != SGM_OK) return rc;
@@ -1121,6 +1155,8 @@ int sgm_create(const sgm_params *p, int device, sgm_handle **out) {
             slant_forced = e && *e == '1';
             const bool want = e && *e ? slant_forced : slant_default(h->g, h->nviews);
             h->slant = !p->aux_only && p->solver == SGM_SOLVER_SGM && want;
+            const char *ev = getenv("SGM_VSTRIP");
+            h->vstrip = !(ev && *ev == '0');
         }
         const size_t ng = h->slant ? sgm::slant_gran_count(h->g, h->nviews) : 0;
         if (!rc && h->slant) {

@@ -190,12 +190,19 @@ __host__ __device__ constexpr int costh_pad(int D, int scale) { return D / scale
 // LDS, which halves the staging and keeps 4K rows (3840 px) inside 64 KiB.
 // DC: D as a compile-time constant (0: runtime D), so the stores of an
 // unrolled block take immediate offsets instead of a 64-bit address add each
-template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI, int DC = 0>
+// CK > 0 (the strip schedule's checkpoint pass, sgm_vstrip.hip): no volume
+// is written; at every output position p = CK * s (2 <= p <= W-3) the state
+// before the step that produces p -- the running sum and the values at
+// positions p-2, p-1 it will subtract -- goes to out[((i * ck_ns + s) * 3 +
+// k) * D + d], k = 0 .. 2.
+template <int VIEW, int WIN, bool SKY, bool FILTER, bool UNI, int DC = 0, int CK = 0>
 __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
                                             const uint64_t *__restrict__ ctr,
                                             const uint8_t *__restrict__ sky, int sky_pitch, int H,
                                             int W, int D, int scale, int R,
-                                            float *__restrict__ out, int blk, unsigned char *smem) {
+                                            float *__restrict__ out, int blk, unsigned char *smem,
+                                            int ck_ns = 0) {
+    static_assert(CK == 0 || (WIN == 5 && FILTER), "checkpoints of the 5-wide filter");
     const int P = costh_pad(D, scale), RS = W + 2 * P;
     constexpr int NS = UNI ? 1 : 2;  // staged census rows per image row
     uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
@@ -221,7 +228,7 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     const uint64_t *cr = sr + (size_t)r * RS + P - (VIEW == 0 ? ds : 0);
     const uint64_t *cu = (VIEW == 0 ? ctl : ctr) + (size_t)i * W;  // UNI: the uniform row
     const uint8_t *sk = ss + (size_t)r * RS + P;
-    float *o = out + (size_t)i * W * D + d;
+    float *o = out + (CK ? (size_t)i * ck_ns * 3 * D : (size_t)i * W * D) + d;
     const size_t DS = DC ? (size_t)DC : (size_t)D;  // store stride
 
     auto word_l = [&](int j) { return UNI && VIEW == 0 ? cu[j < W - 1 ? j : W - 1] : cl[j]; };
@@ -244,16 +251,29 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
     float sum = 0.0f;
 #pragma unroll
     for (int k = 0; k < WIN; ++k) sum += raw(k);
+    if constexpr (CK == 0) {
 #pragma unroll
-    for (int p = 0; p < LAG; ++p) costh_store(raw(p), o + (size_t)p * DS);
+        for (int p = 0; p < LAG; ++p) costh_store(raw(p), o + (size_t)p * DS);
+    }
     const int T = W - 2 * HALF;
     // hist[0] is what step t subtracts: raw[t] for t < LAG, output t-LAG after
     float hist[LAG > 0 ? LAG : 1];
 #pragma unroll
     for (int p = 0; p < LAG; ++p) hist[p] = raw(p);
+    auto ck_store = [&](int p) {
+        if constexpr (CK > 0) {
+            if (p % CK == 0) {
+                float *q = o + (size_t)(p / CK) * 3 * DS;
+                q[0] = sum;
+                q[DS] = hist[0];
+                q[2 * DS] = hist[LAG - 1];
+            }
+        }
+    };
     auto step = [&](int t, float rw) {
+        ck_store(LAG + t);
         const float v = div_win<WIN>(sum);
-        costh_store(v, o + (size_t)(LAG + t) * DS);
+        if constexpr (CK == 0) costh_store(v, o + (size_t)(LAG + t) * DS);
         sum += rw;
         float a;
         if constexpr (LAG == 0) {
@@ -301,6 +321,10 @@ __device__ __forceinline__ void cost_h_body(const uint64_t *__restrict__ ctl,
         t += U;
     }
     for (; t < T - 1; ++t) step(t, raw(WIN + t));
+    if constexpr (CK > 0) {
+        if (T >= 1) ck_store(LAG + T - 1);
+        return;
+    }
     if (T >= 1) costh_store(div_win<WIN>(sum), o + (size_t)(LAG + T - 1) * DS);
     for (int p = LAG + T; p < W; ++p) costh_store(raw(p), o + (size_t)p * DS);
 }
@@ -478,6 +502,56 @@ hipError_t launch_cost_h2(const uint64_t *ctl, const uint64_t *ctr, const uint8_
     }
     if (g.scale == 1) return launch_cost_h2_t<5, false, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
     return launch_cost_h2_t<2, false, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
+}
+
+// The strip schedule's checkpoint pass (sgm_vstrip.hip): each view slot's
+// horizontal IIR state at every strip edge, both slots in one launch
+// (workgroup z = slot; dsi0/dsi1: the slot's DSI, 0 left view, 1 right).
+template <bool SKY, bool UNI, int DC>
+__global__ __launch_bounds__(256) void cost_ck_kernel(const uint64_t *__restrict__ ctl,
+                                                      const uint64_t *__restrict__ ctr,
+                                                      const uint8_t *__restrict__ sky0,
+                                                      const uint8_t *__restrict__ sky1, int sky_pitch,
+                                                      int H, int W, int D, int R, float *__restrict__ out0,
+                                                      float *__restrict__ out1, int dsi0, int dsi1, int ns) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const bool z = __builtin_amdgcn_workgroup_id_z() != 0;
+    if ((z ? dsi1 : dsi0) == 0)
+        cost_h_body<0, 5, SKY, true, UNI, DC, kVStripNC>(ctl, ctr, z ? sky1 : sky0, sky_pitch, H, W, D, 1, R,
+                                                         z ? out1 : out0, bid_x(), smem, ns);
+    else
+        cost_h_body<1, 5, SKY, true, UNI, DC, kVStripNC>(ctl, ctr, z ? sky1 : sky0, sky_pitch, H, W, D, 1, R,
+                                                         z ? out1 : out0, bid_x(), smem, ns);
+}
+
+template <bool SKY>
+static hipError_t launch_cost_ck_t(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky0,
+                                   const uint8_t *sky1, int sky_pitch, int dsi0, int dsi1, int nviews,
+                                   Geom g, float *ck0, float *ck1, hipStream_t st) {
+    bool uni;
+    int R;
+    size_t smem;
+    costh_shape(g, SKY, uni, R, smem);
+    if (R < 1 || g.scale != 1) return hipErrorInvalidValue;  // (vstrip_supported)
+    const dim3 grid((g.H + R - 1) / R, 1, nviews);
+    const int ns = (int)vstrip_strips(g);
+    // (the staged rows' LDS sets the occupancy; census operands straight from
+    // global memory instead measured slower: HD256 610 vs 317 us, 4K256 2.33
+    // vs 1.82 ms, profiles/r06_experiments/r06q_vstrip.txt)
+#define CK_ARGS ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, R, ck0, ck1, dsi0, dsi1, ns
+    if (uni) cost_ck_kernel<SKY, true, 0><<<grid, R * g.D, smem, st>>>(CK_ARGS);
+    else if (g.D == 128) cost_ck_kernel<SKY, false, 128><<<grid, R * g.D, smem, st>>>(CK_ARGS);
+    else cost_ck_kernel<SKY, false, 0><<<grid, R * g.D, smem, st>>>(CK_ARGS);
+#undef CK_ARGS
+    return hipGetLastError();
+}
+
+hipError_t launch_cost_ck(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky0,
+                          const uint8_t *sky1, int sky_pitch, int dsi0, int dsi1, int nviews, Geom g,
+                          float *ck0, float *ck1, hipStream_t st) {
+    if (nviews == 2 && (sky0 == nullptr) != (sky1 == nullptr)) return hipErrorInvalidValue;
+    if (sky0) return launch_cost_ck_t<true>(ctl, ctr, sky0, sky1, sky_pitch, dsi0, dsi1, nviews, g, ck0, ck1, st);
+    return launch_cost_ck_t<false>(ctl, ctr, sky0, sky1, sky_pitch, dsi0, dsi1, nviews, g, ck0, ck1, st);
 }
 
 hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,

@@ -207,6 +207,29 @@ hipError_t launch_cost_h2(const uint64_t *ctl, const uint64_t *ctr, const uint8_
 hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky,
                          int sky_pitch, int view, int filter, Geom g, float *out,
                          hipStream_t st);
+// The strip schedule of the slanted frames' cost stage (sgm_vstrip.hip):
+// a checkpoint pass of the horizontal IIR (launch_cost_ck, sgm_cost.hip),
+// then one pass writing C and the L3 volume (launch_vstrip).  kVStripNC
+// columns per strip; checkpoints: H x strips x 3 x D floats per view.
+constexpr int kVStripNC = 16;
+struct VStripArgs {
+    const uint64_t *ctl, *ctr;  // census words (left, right image)
+    const uint8_t *sky0, *sky1; // per view slot (null: no mask)
+    int sky_pitch;
+    int dsi0, dsi1;             // slot's DSI: 0 left view, 1 right view
+    const float *ck0, *ck1;     // checkpoints (launch_cost_ck)
+    float *c0, *c1;             // final cost C
+    float *l30, *l31;           // L3 volume
+    float *dummy;               // >= 256 floats: the target of idle stores
+    float p1, p2;
+};
+size_t vstrip_strips(Geom g);
+size_t vstrip_ck_floats(Geom g);
+bool vstrip_supported(Geom g, bool sky);
+hipError_t launch_cost_ck(const uint64_t *ctl, const uint64_t *ctr, const uint8_t *sky0,
+                          const uint8_t *sky1, int sky_pitch, int dsi0, int dsi1, int nviews, Geom g,
+                          float *ck0, float *ck1, hipStream_t st);
+hipError_t launch_vstrip(const VStripArgs &a, int nviews, Geom g, hipStream_t st);
 hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st);
 hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream_t st);
 // post_filter (sgm_post.hip)

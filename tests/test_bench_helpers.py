@@ -75,7 +75,8 @@ FRAME_KERNELS = ("census_kernel<", "cost_h_kernel<", "cost_h2_kernel<", "cost_h_
                  "vfwd_kernel<", "vfwd2_kernel<", "stage_a_kernel<", "stage_a2_kernel<", "stage_b_kernel<",
                  "stage_b2_kernel<", "hpair_kernel<", "sweep_kernel<7", "sweep2_kernel<7",
                  "sweep_split_kernel<7", "pair_final_kernel<", "pair_final2_kernel<", "slant_kernel<",
-                 "lr_kernel(", "lr_cm_kernel(", "lk_refine_kernel(", "median_fill_kernel<")
+                 "lr_kernel(", "lr_cm_kernel(", "lk_refine_kernel(", "median_fill_kernel<",
+                 "cost_ck_kernel<", "vstrip_kernel<")
 
 
 def test_pmc_reducer_names_every_frame_kernel():
@@ -98,5 +99,5 @@ def test_pmc_reducer_names_every_frame_kernel():
             seen.add(short(n))
     # the volume kernels among them carry algorithmic bytes in bench.py
     for k in ("cost_h", "vfwd", "vfwd_l3", "stage_a", "stage_b", "sweep_L8_acc", "pair_bwd_L4_final",
-              "slant_down", "slant_up", "stage_a_h"):
+              "slant_down", "slant_up", "stage_a_h", "cost_ck", "vstrip"):
         assert k in seen and bench.bytes_per_elem(k, 128) > 0, k
