@@ -504,6 +504,112 @@ hipError_t launch_cost_h2(const uint64_t *ctl, const uint64_t *ctr, const uint8_
     return launch_cost_h2_t<2, false, true>(ctl, ctr, sky0, sky1, sky_pitch, g, out0, out1, st);
 }
 
+// The checkpoint pass's chain (sgm_vstrip.hip): cost_h_body's horizontal IIR
+// (WIN = 5, no sky mask), storing only the state at every strip edge.  Its
+// bytes are negligible, so the chains' latency is its time: the steps run in
+// blocks of one strip (U = kVStripNC) that start at an edge, so the
+// checkpoint is the block's first action (no branch), and the next block's
+// census words are loaded one block ahead -- the uniform row (UNI) by vector
+// loads from an opaque per-lane address: SMEM returns out of order, so its
+// waits are lgkmcnt(0), which hipcc placed right before each block.
+template <int VIEW, bool UNI>
+__device__ __forceinline__ void cost_ck_body(const uint64_t *__restrict__ ctl,
+                                             const uint64_t *__restrict__ ctr, int H, int W, int D,
+                                             int R, float *__restrict__ out, int blk,
+                                             unsigned char *smem, int ns) {
+    constexpr int U = kVStripNC;
+    const int P = costh_pad(D, 1), RS = W + 2 * P;
+    constexpr int NS = UNI ? 1 : 2;
+    uint64_t *sl = reinterpret_cast<uint64_t *>(smem);
+    uint64_t *sr = sl + (UNI ? 0 : (size_t)R * RS);
+    const int row0 = blk * R;
+    for (int idx = tid_x(); idx < R * RS; idx += R * D) {
+        const int r = idx / RS, jp = idx - r * RS, i = row0 + r;
+        const int j = clampi(jp - P, 0, W - 1);
+        if (i < H) {
+            if (!UNI || VIEW == 1) sl[idx] = ctl[(size_t)i * W + j];
+            if (!UNI || VIEW == 0) sr[idx] = ctr[(size_t)i * W + j];
+        }
+    }
+    (void)NS;
+    __syncthreads();
+    const int r = UNI ? uniform(tid_x() / D) : tid_x() / D, d = tid_x() - r * D;
+    const int i = row0 + r;
+    if (i >= H) return;
+    const uint64_t *cl = sl + (size_t)r * RS + P + (VIEW == 1 ? d : 0);
+    const uint64_t *cr = sr + (size_t)r * RS + P - (VIEW == 0 ? d : 0);
+    const uint64_t *cu = (VIEW == 0 ? ctl : ctr) + (size_t)i * W;
+#ifdef COSTCK_VLOAD
+    if constexpr (UNI) {
+        int z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        cu += z;
+    }
+#endif
+    float *o = out + (size_t)i * ns * 3 * D + d;
+    // the shifted operand (LDS) and the other one (UNI: global) of position
+    // j <= W-1 (positions past the row are clamped; their costs feed nothing)
+    auto wu = [&](int j) { return UNI ? cu[j] : (VIEW == 0 ? cl[j] : cr[j]); };
+    auto ws = [&](int j) { return VIEW == 0 ? cr[j] : cl[j]; };
+    auto raw = [&](int j) {
+        j = min(j, W - 1);
+        return VIEW == 0 ? hamming(wu(j), ws(j)) : hamming(ws(j), wu(j));
+    };
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) sum += raw(k);
+    float h0 = raw(0), h1 = raw(1);
+    const int T = W - 4;  // steps: output position t+2; steps t < T-1 update
+    auto step = [&](float rw) {
+        const float v = div_win<5>(sum);
+        sum += rw;
+        sum -= h0;
+        h0 = h1;
+        h1 = v;
+    };
+    auto ck_store = [&](int s) {
+        float *q = o + (size_t)s * 3 * D;
+        q[0] = sum;
+        q[D] = h0;
+        q[2 * D] = h1;
+    };
+    // a step with its conditions (the prologue and the tail): the checkpoint
+    // of the strip starting at position t+2, then the update
+    auto gstep = [&](int t) {
+        if ((t + 2) % U == 0) ck_store((t + 2) / U);
+        if (t < T - 1) step(raw(t + 5));
+    };
+    int t = 0;
+    for (; t < U - 2 && t < T; ++t) gstep(t);
+    // full blocks b (steps U*b-2 .. U*b+U-3, all updating): U*(b+1) - 2 < T
+    int b = 1;
+    if (U * (b + 1) - 2 < T) {
+        float cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = raw(U * b + 3 + u);
+        for (; U * (b + 1) - 2 < T; ++b) {
+            uint64_t nu[U], nw[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = min(U * (b + 1) + 3 + u, W - 1);
+                nu[u] = wu(j);
+                nw[u] = ws(j);
+            }
+            // (scheduling fences: else hipcc pulls each word's hamming up next
+            // to its load and waits for it inside the chain)
+            __builtin_amdgcn_sched_barrier(0);
+            ck_store(b);
+#pragma unroll
+            for (int u = 0; u < U; ++u) step(cur[u]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = VIEW == 0 ? hamming(nu[u], nw[u]) : hamming(nw[u], nu[u]);
+        }
+        t = U * b - 2;
+    }
+    for (; t < T; ++t) gstep(t);
+}
+
 // The strip schedule's checkpoint pass (sgm_vstrip.hip): each view slot's
 // horizontal IIR state at every strip edge, both slots in one launch
 // (workgroup z = slot; dsi0/dsi1: the slot's DSI, 0 left view, 1 right).
@@ -516,12 +622,16 @@ __global__ __launch_bounds__(256) void cost_ck_kernel(const uint64_t *__restrict
                                                       float *__restrict__ out1, int dsi0, int dsi1, int ns) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const bool z = __builtin_amdgcn_workgroup_id_z() != 0;
-    if ((z ? dsi1 : dsi0) == 0)
+    if constexpr (!SKY) {
+        if ((z ? dsi1 : dsi0) == 0) cost_ck_body<0, UNI>(ctl, ctr, H, W, D, R, z ? out1 : out0, bid_x(), smem, ns);
+        else cost_ck_body<1, UNI>(ctl, ctr, H, W, D, R, z ? out1 : out0, bid_x(), smem, ns);
+    } else if ((z ? dsi1 : dsi0) == 0) {
         cost_h_body<0, 5, SKY, true, UNI, DC, kVStripNC>(ctl, ctr, z ? sky1 : sky0, sky_pitch, H, W, D, 1, R,
                                                          z ? out1 : out0, bid_x(), smem, ns);
-    else
+    } else {
         cost_h_body<1, 5, SKY, true, UNI, DC, kVStripNC>(ctl, ctr, z ? sky1 : sky0, sky_pitch, H, W, D, 1, R,
                                                          z ? out1 : out0, bid_x(), smem, ns);
+    }
 }
 
 template <bool SKY>
