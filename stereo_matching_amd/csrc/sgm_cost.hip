@@ -645,9 +645,10 @@ static hipError_t launch_cost_ck_t(const uint64_t *ctl, const uint64_t *ctr, con
     if (R < 1 || g.scale != 1) return hipErrorInvalidValue;  // (vstrip_supported)
     const dim3 grid((g.H + R - 1) / R, 1, nviews);
     const int ns = (int)vstrip_strips(g);
-    // (the staged rows' LDS sets the occupancy; census operands straight from
-    // global memory instead measured slower: HD256 610 vs 317 us, 4K256 2.33
-    // vs 1.82 ms, profiles/r06_experiments/r06q_vstrip.txt)
+    // (census operands straight from global memory instead of the staged
+    // rows measured slower: HD256 610 vs 317 us, 4K256 2.33 vs 1.82 ms; one
+    // row per block, for more waves per CU, changed nothing:
+    // profiles/r06_experiments/r06q_vstrip.txt)
 #define CK_ARGS ctl, ctr, sky0, sky1, sky_pitch, g.H, g.W, g.D, R, ck0, ck1, dsi0, dsi1, ns
     if (uni) cost_ck_kernel<SKY, true, 0><<<grid, R * g.D, smem, st>>>(CK_ARGS);
     else if (g.D == 128) cost_ck_kernel<SKY, false, 128><<<grid, R * g.D, smem, st>>>(CK_ARGS);
