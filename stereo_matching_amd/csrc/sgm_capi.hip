@@ -788,6 +788,8 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
     const uint8_t *sky0 = right_only ? d_sky_r : d_sky_l;
     const bool vstrip = h->slant && h->vstrip && sgm::vstrip_supported(g, sky0 != nullptr) &&
                         (h->nviews == 1 || (sky0 == nullptr) == (d_sky_r == nullptr));
+    // (a masked frame's sky flags go to the strip pass as words, after the
+    // checkpoints in the Ch buffer: 3/16 + 2/D of its floats at most)
     if (vstrip) {
         const int dsi0 = right_only ? 1 : 0;
         HIPCHK(h, timed(h, "cost_ck", h->nviews * npx * g.D, st, [&] {
@@ -797,9 +799,17 @@ int run_frame(sgm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int 
         sgm::VStripArgs va{};
         va.ctl = h->d_ct[0];
         va.ctr = h->d_ct[1];
-        va.sky0 = sky0;
-        va.sky1 = d_sky_r;
-        va.sky_pitch = sky_pitch;
+        if (sky0) {
+            const uint8_t *skm[2] = {sky0, d_sky_r};
+            uint64_t *skw[2] = {nullptr, nullptr};
+            for (int v = 0; v < h->nviews; ++v) {
+                skw[v] = reinterpret_cast<uint64_t *>(h->d_ch[v] + sgm::vstrip_sky_words_offset(g));
+                HIPCHK(h, timed(h, "sky_words", npx, st,
+                                [&] { return sgm::launch_sky_words(skm[v], sky_pitch, g, skw[v], st); }));
+            }
+            va.skw0 = skw[0];
+            va.skw1 = skw[1];
+        }
         va.dsi0 = dsi0;
         va.dsi1 = 1;
         va.ck0 = h->d_ch[0];  // (the checkpoints sit in the dead Ch volumes)

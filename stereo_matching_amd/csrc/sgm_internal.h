@@ -214,8 +214,7 @@ hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t
 constexpr int kVStripNC = 16;
 struct VStripArgs {
     const uint64_t *ctl, *ctr;  // census words (left, right image)
-    const uint8_t *sky0, *sky1; // per view slot (null: no mask)
-    int sky_pitch;
+    const uint64_t *skw0, *skw1; // per view slot: sky flags, one word per pixel (null: no mask)
     int dsi0, dsi1;             // slot's DSI: 0 left view, 1 right view
     const float *ck0, *ck1;     // checkpoints (launch_cost_ck)
     float *c0, *c1;             // final cost C
@@ -230,6 +229,10 @@ hipError_t launch_cost_ck(const uint64_t *ctl, const uint64_t *ctr, const uint8_
                           const uint8_t *sky1, int sky_pitch, int dsi0, int dsi1, int nviews, Geom g,
                           float *ck0, float *ck1, hipStream_t st);
 hipError_t launch_vstrip(const VStripArgs &a, int nviews, Geom g, hipStream_t st);
+// the sky mask as 0/1 words (the strip pass stages 8-byte words only), kept
+// in the Ch buffer after the checkpoints (offset in floats)
+size_t vstrip_sky_words_offset(Geom g);
+hipError_t launch_sky_words(const uint8_t *sky, int pitch, Geom g, uint64_t *out, hipStream_t st);
 hipError_t launch_copy(const float *in, float *out, Geom g, hipStream_t st);
 hipError_t launch_sweep(int dir, int mode, const SweepArgs &a, Geom g, hipStream_t st);
 // post_filter (sgm_post.hip)

@@ -30,11 +30,12 @@
 namespace sgm {
 
 // A row's staged census (double-buffered): the shifted image's words, the
-// other image's (one per column), one dummy word for the idle lanes (every
-// thread stores one word: no branches).
+// other image's (one per column), the sky flags (one word per column, from
+// the sky-word array launch_sky_words writes), one dummy word for the idle
+// lanes (every thread stores one word: no branches).
 template <int V, int NC>
 struct VStripStage {
-    static constexpr int NSH = NC + 3 + 64 * V, UN = NSH, N = UN + NC + 3 + 1;
+    static constexpr int NSH = NC + 3 + 64 * V, UN = NSH, SK = UN + NC + 3, N = SK + NC + 3 + 1;
 };
 template <int V, int NC>
 struct VStripLds {
@@ -77,25 +78,27 @@ __global__ __launch_bounds__(64 * (NH + NV)) void vstrip_kernel(VStripArgs a, Ge
     // words for columns j0 - D + 1 .. j0 + NC + 2 (left-view DSI: the right
     // image at j - d, clamped at 0) or j0 .. j0 + NC + D + 1 (right-view DSI:
     // the left image at j + d, clamped at W-1) and the other image's for
-    // columns j0 .. j0 + NC + 2 (clamped at W-1).  Loads run PD rows ahead of
-    // their LDS store through a register ring; every thread loads one word
-    // from a valid address, no branches (a branch around a load makes the
-    // waitcnt pass drain the ring).  (No sky mask: a masked frame's raw costs
-    // need a byte per pixel, whose load the compiler's zero-extension waits
-    // for at once; such frames run cost_h + vfwd_l3.)
+    // columns j0 .. j0 + NC + 2 (clamped at W-1), and their sky flags.  Loads
+    // run PD rows ahead of their LDS store through a register ring; every
+    // thread loads one 8-byte word from a valid address, no branches (a branch
+    // around a load makes the waitcnt pass drain the ring).  The sky mask comes
+    // as words too (launch_sky_words): a byte load's zero-extension, which
+    // hipcc scheduled right after its issue, waited for every load in flight.
     const int nsh = NC + 2 + D;
     const int sbase = dsi == 0 ? j0 - D + 1 : j0;
     const uint64_t *shimg = dsi == 0 ? a.ctr : a.ctl, *unimg = dsi == 0 ? a.ctl : a.ctr;
     using SG = VStripStage<V, NC>;
     const int x = tid_x();
-    const int kind = x < nsh ? 0 : (x < nsh + NR ? 1 : 2);
-    const int xi = kind == 0 ? x : x - nsh;
+    const uint64_t *skw = slot ? a.skw1 : a.skw0;
+    const int kind = x < nsh ? 0 : (x < nsh + NR ? 1 : (x < nsh + 2 * NR ? 2 : 3));
+    const int xi = kind == 0 ? x : (kind == 1 ? x - nsh : (kind == 2 ? x - nsh - NR : 0));
     const int scol = kind == 0 ? min(max(sbase + xi, 0), W - 1) : min(j0 + xi, W - 1);
-    const int sidx = kind == 0 ? xi : (kind == 1 ? SG::UN + xi : SG::N - 1);
-    const uint64_t *wsrc = (kind == 0 ? shimg : unimg) + scol;
+    const int sidx = kind == 0 ? xi : (kind == 1 ? SG::UN + xi : (kind == 2 ? SG::SK + xi : SG::N - 1));
+    const bool nosky = kind == 2 && skw == nullptr;  // (its lanes load a census word, store 0)
+    const uint64_t *wsrc = (kind == 0 ? shimg : (kind == 2 && skw ? skw : unimg)) + scol;
     uint64_t rw_[PD];
     auto stage_load = [&](int u, int r) { rw_[u] = wsrc[(size_t)uniform(min(r, H - 1)) * W]; };
-    auto stage_store = [&](int b, int u) { L.st[b][sidx] = rw_[u]; };
+    auto stage_store = [&](int b, int u) { L.st[b][sidx] = nosky ? 0ull : rw_[u]; };
     // rows 0 and 1 to stage buffers 0 and 1; the ring then holds rows 2 .. PD+1
 #pragma unroll
     for (int u = 0; u < PD; ++u) stage_load(u, u);
@@ -213,9 +216,14 @@ __global__ __launch_bounds__(64 * (NH + NV)) void vstrip_kernel(VStripArgs a, Ge
             if (xx < NR) {
                 const uint64_t *sw = &L.st[b][xx + sh0];
                 const uint64_t un = L.st[b][SG::UN + xx];
+                const bool sk = L.st[b][SG::SK + xx] != 0;
                 float r[V];
 #pragma unroll
-                for (int v = 0; v < V; ++v) r[v] = hamming(un, sw[dsi == 0 ? V - 1 - v : v]);
+                for (int v = 0; v < V; ++v) {
+                    // the sky override of Solver.cpp:165-178
+                    const float c = hamming(un, sw[dsi == 0 ? V - 1 - v : v]);
+                    r[v] = sk ? (e0 + v == 0 ? 0.0f : 999999.0f) : c;
+                }
                 store_lds_v<V>(&L.raw[b][xx][e0], r);
             }
         }
@@ -312,7 +320,26 @@ __global__ __launch_bounds__(64 * (NH + NV)) void vstrip_kernel(VStripArgs a, Ge
         if (it0 + u < NIT) iter(it0 + u, u);
 }
 
-bool vstrip_supported(Geom g, bool sky) { return g.scale == 1 && !sky && cost_h2_supported(g, false); }
+bool vstrip_supported(Geom g, bool sky) { return g.scale == 1 && cost_h2_supported(g, sky); }
+
+// The sky mask as one word per pixel (0 or 1) for the strip pass's staging.
+__global__ __launch_bounds__(256) void sky_words_kernel(const uint8_t *__restrict__ sky, int pitch, int H,
+                                                         int W, uint64_t *__restrict__ out) {
+    const size_t n = (size_t)H * W;
+    for (size_t k = (size_t)bid_x() * 256 + tid_x(); k < n; k += (size_t)gridDim.x * 256) {
+        const size_t i = k / W, j = k - i * W;
+        out[k] = sky[i * pitch + j] == 255 ? 1ull : 0ull;
+    }
+}
+
+size_t vstrip_sky_words_offset(Geom g) { return (vstrip_ck_floats(g) + 1) & ~(size_t)1; }
+
+hipError_t launch_sky_words(const uint8_t *sky, int pitch, Geom g, uint64_t *out, hipStream_t st) {
+    const size_t n = (size_t)g.H * g.W;
+    const unsigned blocks = (unsigned)min((n + 255) / 256, (size_t)4096);
+    sky_words_kernel<<<blocks, 256, 0, st>>>(sky, pitch, g.H, g.W, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_vstrip(const VStripArgs &a, int nviews, Geom g, hipStream_t st) {
     const dim3 grid((unsigned)vstrip_strips(g), nviews);

@@ -9,9 +9,8 @@ filter's boundary columns meet the strips: W below, at and just above one
 strip, a strip starting at W-3 (its first column is the last filtered one,
 read from a checkpoint with no update after it), at W-2 and W-1 (raw columns
 only), the 3-row and 5-column minimum frame, each D, one and two views, the
-right-view handle, and the frames where the strip pass does not apply and
-the two-pass path runs: scale 2, and sky masks (the strip pass would need a
-mask byte per pixel per row)."""
+right-view handle, sky masks (staged as one word per pixel), and scale 2,
+where the strip pass does not apply and the two-pass path runs."""
 from __future__ import annotations
 
 import os
@@ -34,9 +33,9 @@ CASES = [
     (10, 27, 1, 256, 2, False),   # strip 1 starts at W-3 (checkpoint, no update)
     (11, 28, 1, 256, 1, False),   # strip 1 starts at W-4
     (33, 300, 1, 32, 2, False),
-    (20, 70, 1, 64, 2, True),     # sky masks: the two-pass path
+    (20, 70, 1, 64, 2, True),     # sky masks
     (40, 97, 1, 64, 2, True),
-    (64, 200, 1, 256, 2, False),
+    (64, 200, 1, 256, 2, True),
     (50, 241, 1, 128, 1, False),
     (40, 100, 2, 64, 2, True),    # scale 2: the two-pass path
 ]
@@ -68,7 +67,7 @@ def _run(c, env, view="left"):
 def test_strips_vs_oracle_and_two_pass(c):
     h, w, s, D, views, _ = c
     m, raw, prof, (left, right, sky) = _run(c, {"SGM_SLANT": "1"})
-    strips = s == 1 and not c[5]
+    strips = s == 1
     assert ("vstrip" in prof) == strips and ("vfwd_l3" in prof) == (not strips), sorted(prof)
     ref = oracle.process(left, right, D, scale=s, sky_l=sky, sky_r=sky, views=views)
     want = ref["lr"] if views == 2 else ref["sub"]
@@ -80,8 +79,8 @@ def test_strips_vs_oracle_and_two_pass(c):
     assert np.array_equal(raw, raw2)
 
 
-@pytest.mark.parametrize("c", [(30, 130, 1, 128, 1, False), (12, 49, 1, 256, 1, False)],
-                         ids=["130_D128", "49_D256"])
+@pytest.mark.parametrize("c", [(30, 130, 1, 128, 1, True), (12, 49, 1, 256, 1, False)],
+                         ids=["130_D128_sky", "49_D256"])
 def test_right_view_handle(c):
     # a right-view handle runs the right-view DSI in slot 0 (dsi0 = 1)
     m, raw, prof, _ = _run(c, {"SGM_SLANT": "1"}, view="right")
