@@ -211,7 +211,10 @@ hipError_t launch_cost_h(const uint64_t *ctl, const uint64_t *ctr, const uint8_t
 // a checkpoint pass of the horizontal IIR (launch_cost_ck, sgm_cost.hip),
 // then one pass writing C and the L3 volume (launch_vstrip).  kVStripNC
 // columns per strip; checkpoints: H x strips x 3 x D floats per view.
-constexpr int kVStripNC = 16;
+#ifndef VSTRIP_NC
+#define VSTRIP_NC 16
+#endif
+constexpr int kVStripNC = VSTRIP_NC;
 struct VStripArgs {
     const uint64_t *ctl, *ctr;  // census words (left, right image)
     const uint64_t *skw0, *skw1; // per view slot: sky flags, one word per pixel (null: no mask)
