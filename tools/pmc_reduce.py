@@ -19,6 +19,7 @@ NAMES = [("hpair_kernel", "stage_a_h"), ("stage_a_kernel", "stage_a"), ("stage_b
          ("pair_final_kernel", "pair_bwd_L4_final"), ("pair_final2_kernel", "pair_bwd_L4_final"),
          ("vfwd_kernel", "vfwd"), ("cost_h_kernel", "cost_h"), ("cost_h2_kernel", "cost_h"),
          ("cost_h_global_kernel", "cost_h"), ("cost_ck_kernel", "cost_ck"), ("vstrip_kernel", "vstrip"),
+         ("sky_words_kernel", "sky_words"),
          ("census_kernel", "census"), ("lr_kernel", "lr"), ("lr_cm_kernel", "lr"), ("sweep_kernel<7", "sweep_L8_acc"),
          ("sweep_split_kernel<7", "sweep_L8_acc"),
          ("median_fill_kernel", "post_median"), ("cc_local_kernel", "post_cc_local"),
