@@ -135,8 +135,10 @@ def test_slant_default_by_size(views, monkeypatch):
     # slanted passes run once every workgroup gets 0.5 full-height tiles of
     # work (views x W >= 0.5 x 14 x CUs; on a 256-CU MI355X HD256 with two
     # views, 3840 >= 1792, and with one view, 1920: both slanted since round
-    # 6's dataflow passes), else the bands.  The expectation uses the
-    # device's own CU count, as the library does.
+    # 6's dataflow passes), else the bands; re-checked on the strip pass
+    # (profiles/r06_experiments/r06r_sizes_vstrip.txt: HD256 one view -3.8%,
+    # 720p D = 256 two views -10.9%).  The expectation uses the device's own
+    # CU count, as the library does.
     import torch
     monkeypatch.delenv("SGM_SLANT", raising=False)
     h, w, D = 1080, 1920, 256
