@@ -423,7 +423,17 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
         pmin = nmin;
         if constexpr (DIAG) cc.advance_if(cpos >= 0, W, D, WD);
         ++cpos;
-        if (refill) refetch(cb[u]);
+        // Rows (FD 0) refill the ring in bursts of RB slots: every RB-th step
+        // reloads the RB slots consumed since the last burst, one contiguous
+        // RB * D-float block of the row (K128 stage A -2.5%, the frame
+        // -0.6..-0.8% paired; HD/4K unchanged; diagonals in bursts were
+        // slower: profiles/r06_experiments/r06t_row_bursts.txt)
+        constexpr int RB = FD == 0 ? 8 : 1;
+        static_assert(PF % RB == 0, "bursts of whole ring slots");
+        if (refill && u % RB == RB - 1) {
+#pragma unroll
+            for (int q = RB - 1; q >= 0; --q) refetch(cb[u - q]);
+        }
     };
     const int total = ke - s0;  // nseg * K for the whole chain
     int k0 = 0;
