@@ -327,7 +327,7 @@ __device__ __forceinline__ void sweep_split_body(const SweepArgs &a, const Geom 
 // BAND (FD 5, the forward bands above the Infinity Cache): steps [kb, ke)
 // of the chain, whole segments (kb, ke = r0 mod K, or ke = n), the state
 // entering the band from a.band.carry and the state leaving it stored there.
-template <int FD, int V, bool FULL, int PF, bool BAND = false>
+template <int FD, int V, bool FULL, int PF, bool BAND = false, bool NTC = false>
 __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, int path) {
 #ifdef SGM_STAMPS
     const long long st_t0 = __builtin_amdgcn_s_memtime();
@@ -375,7 +375,8 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     auto fetch = [&](float (&dst)[V]) {
         if constexpr (FD == 0) {
             const float *src = ppos >= 0 ? hrow + (size_t)ppos * g.D : a.zero;
-            load_v<V>(dst, src + e0, active);
+            if constexpr (NTC) load_v_nt<V>(dst, src + e0, active);
+            else load_v<V>(dst, src + e0, active);
         } else {
             const float *src = ppos >= 0 ? a.cost + pc.off : a.zero;
             load_v<V>(dst, src + e0, active);
@@ -390,7 +391,8 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
     const float *hnext = hrow + (size_t)ppos * g.D + e0;
     auto refetch = [&](float (&dst)[V]) {
         if constexpr (FD == 0) {
-            load_v<V>(dst, hnext, active);
+            if constexpr (NTC) load_v_nt<V>(dst, hnext, active);
+            else load_v<V>(dst, hnext, active);
             hnext += g.D;
         } else {
             fetch(dst);
@@ -454,7 +456,7 @@ __device__ __forceinline__ void pair_fwd_body(const PairArgs &a, const Geom &g, 
 
 // tb/pb: the FINAL mode's LDS ring (two chunks of K total-cost rows and
 // pixel positions), unused otherwise.
-template <int FAM, int V, bool FULL, int MODE, bool BAND = false>
+template <int FAM, int V, bool FULL, int MODE, bool BAND = false, bool NTC = false>
 __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, int path,
                                               float (*tb)[family_k<FAM, V>()][tbuf_stride<V>()],
                                               long long (*pb)[family_k<FAM, V>()]) {
@@ -540,7 +542,8 @@ __device__ __forceinline__ void pair_bwd_body(const PairArgs &a, const Geom &g, 
         fc.init_at(path, pos0, H, W, g.D);
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
-            load_v<V>(cs[kk], a.cost + fc.off + e0, active);
+            if constexpr (NTC) load_v_nt<V>(cs[kk], a.cost + fc.off + e0, active);
+            else load_v<V>(cs[kk], a.cost + fc.off + e0, active);
             fc.advance_if(kk >= K - cnt && fc.k < n - 1, W, D, WD);
         }
         // slot K: the checkpoint seeding the segment, fetched with its costs

@@ -151,9 +151,13 @@ __global__ __launch_bounds__(64) void hpair_kernel(PairArgs h1a, PairArgs h2a, P
     const bool vb = __builtin_amdgcn_workgroup_id_y() != 0;
     const PairArgs h1 = vb ? h1b : h1a;
     const PairArgs h2 = vb ? h2b : h2a;
-    pair_fwd_body<0, V, FULL, PFH>(h1, g, bid_x());
+    // C is read by non-temporal loads (NTC): the H pair runs only above the
+    // Infinity Cache, where its two reads of C pass through once each (the
+    // top-down pass beside it -2.6%, HD256 frame -1.0%, 4K256 -0.6% paired,
+    // profiles/r06_experiments/r06x_hpair_nt.txt)
+    pair_fwd_body<0, V, FULL, PFH, false, true>(h1, g, bid_x());
     __threadfence();  // this wave's checkpoint stores, before it reads them back
-    pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2>(h2, g, bid_x(), nullptr, nullptr);
+    pair_bwd_body<PAIR_H, V, FULL, PAIR_INIT2, false, true>(h2, g, bid_x(), nullptr, nullptr);
 }
 
 // Stage B blocks are two waves: an H block splits its row's L2 pass into a
