@@ -533,11 +533,17 @@ __global__ __launch_bounds__(64 * (NW + 1)) void slant_kernel(SlantArgs a, Geom 
         int pfs = s_begin;  // step of the next ring refill
         auto refill = [&](int slot) {
             const long long o = off_of(pfs);
-            load_v<V>(rb[0][slot], sv.cost + o, dact);
+            // the bottom-up pass is C's last reader: non-temporal like its
+            // other streams (slant_up -0.9% at HD256, -0.4% at 4K256; the
+            // top-down pass's C reads stay default-policy, measured slower
+            // non-temporal: profiles/r06_experiments/r06y_slant_nt.txt)
             if constexpr (UP) {
+                load_v_nt<V>(rb[0][slot], sv.cost + o, dact);
                 load_v_nt<V>(rb[1][slot], sv.s12 + o, dact);
                 load_v_nt<V>(rb[2][slot], sv.l3 + o, dact);
                 load_v_nt<V>(rb[3][slot], sv.t56 + o, dact);
+            } else {
+                load_v<V>(rb[0][slot], sv.cost + o, dact);
             }
             ++pfs;
         };
