@@ -690,7 +690,7 @@ struct SplitFinalLds {
 // loads in flight while one is recomputed); RH: the consumer's ring of
 // accumulator loads is RH*K steps deep (chunks processed RH at a time).
 template <int FAM, int V, bool FULL, int MODE, int K, int NB = 2, int RH = 1, int NWTA = 1,
-          bool BAND = false>
+          bool BAND = false, bool NTC = false>
 __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g, int path,
                                                 int wave, SplitLds<K, V> &L,
                                                 SplitFinalLds<K, V> *F) {
@@ -772,7 +772,8 @@ __device__ __forceinline__ void pair_split_body(const PairArgs &a, const Geom &g
 #pragma unroll
                 for (int kk = 0; kk < K; ++kk) {
                     const int rel = kk - sh > 0 ? kk - sh : 0;
-                    load_v<V>(cs[kk], p0 + (long long)rel * lin_st, active);
+                    if constexpr (NTC) load_v_nt<V>(cs[kk], p0 + (long long)rel * lin_st, active);
+                    else load_v<V>(cs[kk], p0 + (long long)rel * lin_st, active);
                 }
             } else {
                 Cursor<FD> fc;

@@ -97,6 +97,8 @@ struct PairArgs {
                          // that align forward passes with their checkpoints
     float p1, p2, uniq;
     Band band;           // backward passes (D2 ACC, V FINAL): steps in whole segments
+    int nt_cost;         // V FINAL (whole volume): read C by non-temporal loads -- the
+                         // last read of a view's C when the other view's follows
 };
 
 // floats of checkpoint storage a family needs

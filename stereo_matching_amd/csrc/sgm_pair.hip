@@ -71,8 +71,10 @@ __global__ __launch_bounds__(64) void pair_bwd_kernel(PairArgs a, Geom g) {
 template <int V, bool FULL>
 constexpr int final_nwta() { return FULL ? 2 : 1; }
 
-// BAND: one band of the banded backward phase (a.band)
-template <int V, bool FULL, bool BAND = false>
+// BAND: one band of the banded backward phase (a.band).  NTC: C by
+// non-temporal loads (a.nt_cost: two-view frames, whose views' cost volumes
+// alternate in the Infinity Cache; profiles/r06_experiments/r06aa_final_nt.txt)
+template <int V, bool FULL, bool BAND = false, bool NTC = false>
 __global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {
     constexpr int K = pair_kv<V>();
     __shared__ __attribute__((aligned(16))) SplitFinalLds<K, V> lds;
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256) void pair_final_kernel(PairArgs a, Geom g) {
     // row-major output maps (one-view frames): a line's columns on one XCD
     const int path = a.sub_cm ? bid_x() : xcd_column(bid_x(), g.W);
 #endif
-    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>(), BAND>(
+    pair_split_body<PAIR_V, V, FULL, PAIR_FINAL, K, 3, 2, final_nwta<V, FULL>(), BAND, NTC>(
         a, g, path, wave_id(), lds.s, &lds);
 }
 
@@ -370,17 +372,18 @@ static void launch_bwd_t(const PairArgs &a, Geom g, hipStream_t st) {
     else pair_bwd_kernel<FAM, 4, true, MODE><<<grid, 64, 0, st>>>(a, g);
 }
 
-template <bool BAND>
+template <bool BAND, bool NTC = false>
 static void launch_final_b(const PairArgs &a, Geom g, hipStream_t st) {
     const dim3 grid(g.W);
-    if (g.D == 32) pair_final_kernel<1, false, BAND><<<grid, 64 * (2 + final_nwta<1, false>()), 0, st>>>(a, g);
-    else if (g.D == 64) pair_final_kernel<1, true, BAND><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a, g);
-    else if (g.D == 128) pair_final_kernel<2, true, BAND><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a, g);
-    else pair_final_kernel<4, true, BAND><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a, g);
+    if (g.D == 32) pair_final_kernel<1, false, BAND, NTC><<<grid, 64 * (2 + final_nwta<1, false>()), 0, st>>>(a, g);
+    else if (g.D == 64) pair_final_kernel<1, true, BAND, NTC><<<grid, 64 * (2 + final_nwta<1, true>()), 0, st>>>(a, g);
+    else if (g.D == 128) pair_final_kernel<2, true, BAND, NTC><<<grid, 64 * (2 + final_nwta<2, true>()), 0, st>>>(a, g);
+    else pair_final_kernel<4, true, BAND, NTC><<<grid, 64 * (2 + final_nwta<4, true>()), 0, st>>>(a, g);
 }
 
 static void launch_final_t(const PairArgs &a, Geom g, hipStream_t st) {
     if (a.band.ke > 0) launch_final_b<true>(a, g, st);
+    else if (a.nt_cost) launch_final_b<false, true>(a, g, st);
     else launch_final_b<false>(a, g, st);
 }
 
