@@ -508,9 +508,10 @@ int aggregate_view(sgm_handle *h, int view, const float *cost, float *S, float *
     }
     // two views: each final pass is the last read of its view's C, and the
     // other view's volume follows it into the Infinity Cache, so C goes by
-    // non-temporal loads (K128 two views -0.8% paired; one view, whose next
-    // frame rewrites the same C, loses as much in stage A:
-    // profiles/r06_experiments/r06aa_final_nt.txt)
+    // non-temporal loads (K128 two views -1.0% paired).  With one view the
+    // next frame's stage A loses what the final pass gains, with one C buffer
+    // or two used alternately (profiles/r06_experiments/r06aa_final_nt.txt,
+    // r06bb_c_alternate.txt), so one-view frames keep default loads
     pa.nt_cost = h->nviews == 2;
     HIPCHK(h, pair_bwd(h, sgm::PAIR_V, sgm::PAIR_FINAL, pa, st));
     return SGM_OK;
